@@ -1,0 +1,183 @@
+"""Benchmark: simplex pivots/s and HBM-roofline fraction of the gfx950 engine.
+
+Workload (BASELINE.json `metric`, config 3): dense synthetic LP m=16384,
+n=32768 (tableau 16385 x 49153 fp64 = 6.44 GB), Dantzig pricing, generated on
+the device (splitmix64, seed 20220518). A "step" is one simplex pivot:
+price (argmin over the reduced-cost row) -> ratio test (min over the entering
+column) -> Gauss-Jordan rank-1 update of the whole tableau.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+With N > 1 the tableau is row-block partitioned over N processes (one per
+GPU); per pivot the ranks allgather the ratio candidates and allreduce the
+pivot row over RCCL (strong scaling: the LP is the same for every N).
+
+Rank 0 prints ONE JSON line. `roofline.achieved` = algorithmic bytes of one
+rank-1 update on rank 0 (16 * rows * (N+1): one read + one write of every
+local tableau element) / the update kernel's mean device time, timed with HIP
+events on the engine's own stream over the timed region. `cpu_baseline` =
+the CPU oracle (oracle/liblpo.so, same pivot rules, OpenMP) on the same LP,
+rank 0 at N=1 only, for a bounded number of pivots; its pivot sequence is
+compared with the GPU's.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import torch  # noqa: F401  (torch.distributed plumbing; imported first so one HIP runtime serves both)
+import torch.distributed as dist
+
+import linearprogramming_amd as lpg
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+METRIC = "Simplex pivots/sec + HBM GB/s fraction, dense m=16384×n=32768 fp64, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+SEED = 20220518
+CONFIGS = {
+    2: dict(m=1024, n=2048, name="BASELINE config 2: random dense LP m=1024 n=2048 fp64"),
+    3: dict(m=16384, n=32768, name="BASELINE config 3: random dense LP m=16384 n=32768 fp64"),
+    4: dict(m=65536, n=131072, name="BASELINE config 4: random dense LP m=65536 n=131072 fp64"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    ap.add_argument("--variant", type=int, default=None, help="update-kernel variant (LPG_UPDATE_VARIANT)")
+    return ap.parse_args()
+
+
+def cpu_baseline(m, n, gpu_log, budget_s):
+    """Oracle leg: same LP, same rules, OpenMP on the host cores (rank 0, N=1 only)."""
+    from oracle.lpo import GEN_DENSE, RULE_DANTZIG, Oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    o = Oracle(m, n + m + 1, nthreads=threads)
+    o.generate(n, SEED, GEN_DENSE)
+    o.solve(1, RULE_DANTZIG)                       # first pivot untimed (page faults)
+    t0 = time.perf_counter()
+    done = 0
+    while time.perf_counter() - t0 < budget_s and done < 400:
+        o.solve(1, RULE_DANTZIG)
+        done += 1
+    dt = time.perf_counter() - t0
+    k, r = o.get_log()
+    n_cmp = min(len(k), len(gpu_log[0]))
+    same = bool((k[:n_cmp] == gpu_log[0][:n_cmp]).all() and (r[:n_cmp] == gpu_log[1][:n_cmp]).all())
+    o.close()
+    return {"value": done / dt, "unit": "pivots/s", "cores": threads, "kind": "port",
+            "sample": f"{done} timed pivots (after 1 untimed) of the same {m}x{n} LP, oracle/liblpo.so "
+                      f"(C fp64, OpenMP {threads} threads)",
+            "seconds": dt}, {"pivots_compared": int(n_cmp), "identical_pivot_sequence": same}
+
+
+def main():
+    a = parse()
+    if a.variant is not None:
+        os.environ["LPG_UPDATE_VARIANT"] = str(a.variant)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = CONFIGS[a.config]
+    m, n = cfg["m"], cfg["n"]
+    ndev = lpg.device_count()
+    if ndev < 1:
+        raise SystemExit("no GPU visible")
+    dev = local % ndev
+
+    eng = lpg.Engine(m, n + m + 1, device=dev, world=world, rank=rank)
+    if world > 1:
+        uid = [lpg.Engine.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init_rccl(uid[0])
+    eng.generate(n, SEED, lpg.GEN_DENSE)
+    eng.reserve_log(a.warmup + a.steps + 8)
+    eng.enqueue(a.warmup, lpg.RULE_DANTZIG)
+    eng.sync()
+
+    eng.set_timing(True)
+    eng.get_timing()                                   # reset sums
+    if world > 1:
+        dist.barrier()
+    eng.device_sync()
+    t0 = time.perf_counter()
+    eng.enqueue(a.steps, lpg.RULE_DANTZIG)
+    res = eng.sync()
+    eng.device_sync()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    timing = eng.get_timing()
+    info = eng.info
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    upd_ms = timing.update_ms / max(timing.update_count, 1)
+    achieved = info.bytes_per_pivot / (upd_ms * 1e-3) / 1e9 if upd_ms > 0 else 0.0
+    line = {
+        "metric": METRIC,
+        "value": a.steps / elapsed,
+        "unit": "pivots/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": f"synthetic dense LP generated on device (splitmix64 seed {SEED}): A_ij=u, b_i=n/8(1+u), c_j=1+u",
+        "config": {"workload": cfg["name"], "m": m, "n": n, "tableau": [m + 1, n + m + 1],
+                   "tableau_GB": (m + 1) * (n + m + 1) * 8 / 1e9, "rule": "dantzig",
+                   "parallelism": f"row-block x{world}" + (" (RCCL allgather + allreduce per pivot)" if world > 1 else ""),
+                   "update_variant": int(os.environ.get("LPG_UPDATE_VARIANT", "0"))},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "lpg::k_update (Gauss-Jordan rank-1)",
+                     "algorithmic_bytes_per_launch": info.bytes_per_pivot,
+                     "update_ms_mean": upd_ms,
+                     "other_ms_mean": timing.select_ms / max(timing.update_count, 1)},
+        "status": lpg.STATUS_NAMES.get(res.status, res.status),
+        "pivots_total": res.pivots,
+        "objective": res.objective,
+    }
+    pmc = os.path.join(ROOT, "profiles", f"pmc_config{a.config}.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            p = json.load(f)
+        line["roofline"]["traffic"] = p.get("hbm_bytes_per_launch")
+        line["roofline"]["traffic_source"] = os.path.relpath(pmc, ROOT)
+    if world == 1 and rank == 0 and not a.no_cpu:
+        log = eng.get_log()
+        eng.close()
+        cb, parity = cpu_baseline(m, n, log, a.cpu_seconds)
+        line["cpu_baseline"] = cb
+        line["parity"] = parity
+    else:
+        line["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,172 @@
+/*
+ * lpg.h — C-ABI of the MI355X (gfx950) dense-tableau simplex pivot engine.
+ *
+ * This is the drop-in boundary for the pivot loop that the reference
+ * (SomeBottle/LinearProgramming) is missing. The reference's solver driver
+ * `void newSimplex(LPModel *model)` (Source/simplex.h:13, Source/simplex.c:27-73)
+ * builds the tableau with
+ *   `SimplexMatrix CreateSMatrix(LPModel *model, size_t **lack, short int *valid)`
+ *   (Source/matrix.h:23, Source/matrix.c:19-91)
+ * and frees it with `void RevokeSMatrix(SimplexMatrix *)` (matrix.h:25,
+ * matrix.c:97-123) without ever pivoting (the loop belongs between
+ * simplex.c:40 and simplex.c:65). Every entry point below replaces a piece of
+ * that missing loop, or of the SimplexMatrix (matrix.h:13-21) storage it would
+ * have run on; the binding a maintainer adds to simplex.c is in INTEGRATION.md.
+ *
+ * Tableau layout (row-major fp64, same as SimplexMatrix.cMatrix flattened):
+ *   rows 0..m-1  constraint rows  [b_i | a_i1 .. a_iN]   (matrix.c:42-48, 62-66)
+ *   row  m       objective row    [z   | d_1  .. d_N ]   d_j = z_j - c_j
+ *   columns      0 = b, 1..N = variables in LPAlign order (simplex.c:238-260)
+ * The reference maximises (LPStandardize turns min into max, simplex.c:99-106),
+ * so the engine maximises; the optimum is reached when every d_j >= -eps_opt.
+ *
+ * Conventions follow the reference's C style: plain pointers and sizes, caller
+ * owns host buffers (they are copied), the context owns device memory. Return
+ * codes: 0 = success, < 0 = error (lpg_last_error has the text); a host
+ * wrapper maps this onto the reference's `short int valid` (valid = rc == 0).
+ * One context per host thread; not reentrant.
+ *
+ * Multi-GPU: one process per GPU. Each rank creates its context with
+ * lpg_create_dist() and owns the row block [row0, row0 + nrows) of the m
+ * constraint rows (row0 = floor(m*rank/world)); the objective row and the
+ * basis are replicated. Per pivot the ranks exchange, over RCCL/xGMI, the
+ * ratio-test candidates (allgather) and the normalised pivot row (allreduce
+ * of the owner's row and zeros = broadcast from a device-resident root).
+ */
+#ifndef LPG_H
+#define LPG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ---- */
+#define LPG_OK           0
+#define LPG_ERR_ARG     -1
+#define LPG_ERR_DEVICE  -2
+#define LPG_ERR_OOM     -3
+#define LPG_ERR_STATE   -4
+#define LPG_ERR_COMM    -5
+
+/* ---- solve status (SURVEY.md §5 failure detection) ---- */
+#define LPG_RUNNING      0
+#define LPG_OPTIMAL      1
+#define LPG_UNBOUNDED    2
+#define LPG_INFEASIBLE   3
+#define LPG_ITER_LIMIT   4
+#define LPG_NUMERIC      5
+
+/* ---- pricing rules ---- */
+#define LPG_RULE_DANTZIG 0   /* k = argmin d_j, ties -> smallest j; ratio ties -> smallest row */
+#define LPG_RULE_BLAND   1   /* k = min{j : d_j < -eps}; ratio ties -> smallest basic column */
+
+/* ---- synthetic generators (device-side) ---- */
+#define LPG_GEN_DENSE      0  /* A_ij = u, b_i = n/8 (1+u), c_j = 1+u, <= rows, slack basis */
+#define LPG_GEN_DEGENERATE 1  /* lower-triangular KM-style rows, b_i = 0 on even rows     */
+
+/* ---- lpg_create flags ---- */
+#define LPG_FLAG_NO_LOG  0x1u  /* do not record the (entering, leaving) pivot log */
+
+typedef struct lpg_ctx lpg_ctx;
+
+/* Same field layout as oracle/lpo.h's lpo_result. */
+typedef struct {
+    int32_t status;       /* LPG_* status */
+    int32_t rule;         /* rule of the last solve */
+    int64_t pivots;       /* pivots applied so far */
+    double  objective;    /* T[m][0]: z without the objective constant (matrix.c:23-28) */
+    int64_t entering;     /* last pivot's column (1-based, like cMatrix columns), -1 if none */
+    int64_t leaving;      /* last pivot's row (0-based), -1 if none */
+} lpg_result;
+
+typedef struct {
+    int64_t m, ncols, ld;       /* constraint rows, N+1 columns, row pitch (doubles) */
+    int64_t row0, nrows;        /* this rank's constraint-row block */
+    int32_t world, rank, device;
+    int32_t nobj;               /* objective rows (1) */
+    double  bytes_per_pivot;    /* algorithmic HBM bytes of one rank-1 update on this rank:
+                                   16 * (nrows + nobj) * ncols (one read + one write) */
+} lpg_info_t;
+
+typedef struct {
+    double  update_ms;          /* summed device time of the rank-1 update kernel */
+    double  select_ms;          /* summed device time of pricing + ratio-test kernels */
+    double  comm_ms;            /* summed device time of the collectives */
+    int64_t update_count;       /* update launches timed */
+} lpg_timing;
+
+/* Host-staged collectives supplied by the caller (tests, non-RCCL transports).
+ * Buffers are HOST memory; calls block until complete. */
+typedef struct {
+    void *user;
+    int (*allgather)(void *user, const void *send, void *recv, size_t bytes_per_rank);
+    int (*allreduce_sum_f64)(void *user, double *buf, size_t count);
+} lpg_host_comm_ops;
+
+/* ---- lifecycle ---- */
+int  lpg_device_count(int *count);
+/* Single-GPU engine for an m x ncols tableau (ncols = N+1).
+ * Replaces the SimplexMatrix allocation of CreateSMatrix (matrix.c:33-48). */
+int  lpg_create(lpg_ctx **out, int device, int64_t m, int64_t ncols, uint32_t flags);
+/* One rank of a row-block partitioned engine; attach a communicator next. */
+int  lpg_create_dist(lpg_ctx **out, int device, int world, int rank,
+                     int64_t m, int64_t ncols, uint32_t flags);
+int  lpg_comm_unique_id(void *uid, size_t len);              /* RCCL id, len >= 128 */
+int  lpg_comm_init_rccl(lpg_ctx *ctx, const void *uid, size_t len);
+int  lpg_comm_init_host(lpg_ctx *ctx, const lpg_host_comm_ops *ops);
+/* Replaces RevokeSMatrix (matrix.c:97-123). NULL is a no-op. */
+void lpg_destroy(lpg_ctx *ctx);
+int  lpg_info(const lpg_ctx *ctx, lpg_info_t *out);
+const char *lpg_last_error(const lpg_ctx *ctx);
+
+/* ---- loading (host buffers are copied) ---- */
+/* Rows [row0, row0+nrows) in GLOBAL numbering, each [b | a_1..a_N] with pitch
+ * ld >= ncols. Row index m is the objective row. Rows outside this rank's
+ * block are skipped. Replaces CreateSMatrix's cell fill (matrix.c:42-66). */
+int  lpg_load_rows(lpg_ctx *ctx, int64_t row0, int64_t nrows, const double *rows, int64_t ld);
+/* basis[i] = 1-based column of row i's basic variable (all m rows, every
+ * rank). Replaces SimplexMatrix.basicVars (matrix.c:67-78). */
+int  lpg_set_basis(lpg_ctx *ctx, const int64_t *basis);
+/* Objective row from costs c[0..N-1] of `max c.x` and the current basis:
+ * d_j = sum_i c_B(i) T[i][j] - c_j, z = sum_i c_B(i) b_i, summed in global
+ * row order with fma (bitwise independent of the partition). Replaces
+ * SimplexMatrix.ofCosts / basicCosts (matrix.c:55-57, 76-77). */
+int  lpg_set_objective(lpg_ctx *ctx, const double *c);
+int  lpg_set_tolerances(lpg_ctx *ctx, double eps_piv, double eps_opt);
+/* Price only columns 1..nact (e.g. to exclude artificials). */
+int  lpg_set_active_columns(lpg_ctx *ctx, int64_t nact);
+/* Device-side synthetic LP with n structural columns (ncols == n + m + 1). */
+int  lpg_generate(lpg_ctx *ctx, int64_t n, uint64_t seed, int kind);
+
+/* ---- the pivot loop (the part simplex.c:40-65 lacks) ---- */
+/* Pivot until optimal / unbounded / numeric trouble or max_pivots more
+ * pivots; blocks; fills *out. A status of LPG_ITER_LIMIT means the budget
+ * ran out first. */
+int  lpg_solve(lpg_ctx *ctx, int64_t max_pivots, int rule, lpg_result *out);
+/* Asynchronous form for benchmarking: enqueue exactly npivots pivots on the
+ * context's stream without any host synchronisation (pivots after the LP
+ * finishes are no-ops on the device); lpg_sync waits and reports. */
+int  lpg_enqueue(lpg_ctx *ctx, int64_t npivots, int rule);
+int  lpg_sync(lpg_ctx *ctx, lpg_result *out);
+/* Pre-size the device pivot log for npivots more pivots so that no
+ * reallocation (and host synchronisation) happens inside a timed region. */
+int  lpg_reserve_log(lpg_ctx *ctx, int64_t npivots);
+
+/* ---- readout ---- */
+int  lpg_get_rows(lpg_ctx *ctx, int64_t row0, int64_t nrows, double *out, int64_t ld);
+int  lpg_get_basis(lpg_ctx *ctx, int64_t *basis);            /* m entries */
+int  lpg_get_column0(lpg_ctx *ctx, double *xB);               /* local rows' b (x_B) */
+int64_t lpg_get_log(lpg_ctx *ctx, int64_t *k, int64_t *r, int64_t max);
+
+/* ---- measurement ---- */
+int  lpg_set_timing(lpg_ctx *ctx, int enable);
+int  lpg_get_timing(lpg_ctx *ctx, lpg_timing *out);          /* syncs; resets the sums */
+int  lpg_device_sync(lpg_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,101 @@
+"""ctypes binding of include/lpg.h (the C-ABI of the gfx950 pivot engine).
+
+The shared library is built in-tree (``make`` -> linearprogramming_amd/liblpg.so)
+so that it travels with the repository snapshot to the GPU box. There is no
+fallback: if the library is missing or cannot be loaded, importing the engine
+raises, so a GPU test can never pass on a silent CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblpg.so")
+
+# include/lpg.h constants
+OK, ERR_ARG, ERR_DEVICE, ERR_OOM, ERR_STATE, ERR_COMM = 0, -1, -2, -3, -4, -5
+RUNNING, OPTIMAL, UNBOUNDED, INFEASIBLE, ITER_LIMIT, NUMERIC = 0, 1, 2, 3, 4, 5
+STATUS_NAMES = {0: "RUNNING", 1: "OPTIMAL", 2: "UNBOUNDED", 3: "INFEASIBLE", 4: "ITER_LIMIT", 5: "NUMERIC"}
+RULE_DANTZIG, RULE_BLAND = 0, 1
+GEN_DENSE, GEN_DEGENERATE = 0, 1
+FLAG_NO_LOG = 0x1
+
+c_double_p = ctypes.POINTER(ctypes.c_double)
+c_int64_p = ctypes.POINTER(ctypes.c_int64)
+
+
+class Result(ctypes.Structure):
+    """lpg_result (same layout as oracle lpo_result)."""
+    _fields_ = [("status", ctypes.c_int32), ("rule", ctypes.c_int32), ("pivots", ctypes.c_int64),
+                ("objective", ctypes.c_double), ("entering", ctypes.c_int64), ("leaving", ctypes.c_int64)]
+
+
+class Info(ctypes.Structure):
+    _fields_ = [("m", ctypes.c_int64), ("ncols", ctypes.c_int64), ("ld", ctypes.c_int64),
+                ("row0", ctypes.c_int64), ("nrows", ctypes.c_int64),
+                ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("nobj", ctypes.c_int32), ("bytes_per_pivot", ctypes.c_double)]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("update_ms", ctypes.c_double), ("select_ms", ctypes.c_double),
+                ("comm_ms", ctypes.c_double), ("update_count", ctypes.c_int64)]
+
+
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, c_double_p, ctypes.c_size_t)
+
+
+class HostCommOps(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("allgather", ALLGATHER_FN), ("allreduce_sum_f64", ALLREDUCE_FN)]
+
+
+# (name, restype, argtypes) for every function include/lpg.h declares.
+PROTOTYPES = [
+    ("lpg_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    ("lpg_create", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32]),
+    ("lpg_create_dist", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32]),
+    ("lpg_comm_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    ("lpg_comm_init_rccl", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    ("lpg_comm_init_host", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HostCommOps)]),
+    ("lpg_destroy", None, [ctypes.c_void_p]),
+    ("lpg_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Info)]),
+    ("lpg_last_error", ctypes.c_char_p, [ctypes.c_void_p]),
+    ("lpg_load_rows", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, c_double_p, ctypes.c_int64]),
+    ("lpg_set_basis", ctypes.c_int, [ctypes.c_void_p, c_int64_p]),
+    ("lpg_set_objective", ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    ("lpg_set_tolerances", ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_double]),
+    ("lpg_set_active_columns", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    ("lpg_generate", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int]),
+    ("lpg_solve", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(Result)]),
+    ("lpg_enqueue", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]),
+    ("lpg_sync", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Result)]),
+    ("lpg_reserve_log", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    ("lpg_get_rows", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, c_double_p, ctypes.c_int64]),
+    ("lpg_get_basis", ctypes.c_int, [ctypes.c_void_p, c_int64_p]),
+    ("lpg_get_column0", ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    ("lpg_get_log", ctypes.c_int64, [ctypes.c_void_p, c_int64_p, c_int64_p, ctypes.c_int64]),
+    ("lpg_set_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("lpg_get_timing", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Timing)]),
+    ("lpg_device_sync", ctypes.c_int, [ctypes.c_void_p]),
+]
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load liblpg.so and declare every prototype. Raises if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"lpg HIP engine not built: {path} is missing (run `make` or __graft_entry__.build())")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, res, args in PROTOTYPES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

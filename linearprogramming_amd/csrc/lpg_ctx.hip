@@ -1,0 +1,688 @@
+// lpg_ctx.hip — context, memory layout, pivot-loop driver and the extern "C"
+// entry points of include/lpg.h.
+//
+// The host side of one pivot is a fixed sequence of launches on one stream
+// (prep -> [allreduce P] -> [price] -> select -> [allgather candidates] ->
+// update); nothing is read back per pivot, so the host runs ahead of the
+// device and lpg_solve only synchronises every `batch` pivots to check the
+// device-side status (SURVEY.md §3 call stack (3)).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/lpg.h"
+#include "lpg_internal.h"
+
+using namespace lpg;
+
+namespace {
+
+thread_local char g_err[512];
+
+struct TimingRing {
+    std::vector<hipEvent_t> ev;   // 3 per pivot: before prep, before update, after update
+    int used = 0;
+    double update_ms = 0, select_ms = 0, comm_ms = 0;
+    int64_t count = 0;
+};
+
+}  // namespace
+
+struct lpg_ctx {
+    int device = 0, world = 1, rank = 0;
+    int64_t m = 0, ncols = 0, ld = 0, row0 = 0, nloc = 0, nobj = 1, nact = 0;
+    double eps_piv = 1e-9, eps_opt = 1e-9;
+    uint32_t flags = 0;
+    // device buffers
+    double *T = nullptr;          // (nloc + nobj) x ld
+    double *P = nullptr;          // ld
+    double *C[2] = {nullptr, nullptr};
+    double *acc = nullptr;        // ld (objective chain)
+    double *cb = nullptr;         // nloc
+    double *cost = nullptr;       // ncols
+    PricePart *pp = nullptr;
+    Cand *part = nullptr;         // nsel (this rank's select partials)
+    Cand *cand = nullptr;         // world * nsel (gathered); == part when world == 1
+    int64_t *basis = nullptr;     // m (replicated)
+    int64_t *logk = nullptr, *logr = nullptr;
+    int64_t logcap = 0;
+    DevState *st = nullptr;
+    int npp = 0, nsel = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    // pivot-loop host state
+    bool booted = false;
+    int boot_rule = 0;
+    int par = 0;                  // parity of the next pivot's slot
+    int64_t enq = 0;              // pivots enqueued since the last reset (log bound)
+    int update_variant = 0;
+    // communication
+    ncclComm_t nccl = nullptr;
+    lpg_host_comm_ops hops{};
+    bool have_hops = false;
+    std::vector<unsigned char> hsend, hrecv;
+    // timing
+    bool timing = false;
+    TimingRing tr;
+    char err[512] = {0};
+};
+
+static int fail(lpg_ctx *c, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) snprintf(c->err, sizeof c->err, "%s", buf);
+    snprintf(g_err, sizeof g_err, "%s", buf);
+    return code;
+}
+
+#define HIPCHK(c, x)                                                                         \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) return fail((c), LPG_ERR_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+static Geo geo(const lpg_ctx *c) {
+    Geo g;
+    g.T = c->T;
+    g.ld = c->ld;
+    g.nloc = c->nloc;
+    g.nobj = c->nobj;
+    g.ncols = c->ncols;
+    g.nact = c->nact;
+    g.row0 = c->row0;
+    g.m = c->m;
+    g.eps_piv = c->eps_piv;
+    g.eps_opt = c->eps_opt;
+    return g;
+}
+
+static Launch lau(const lpg_ctx *c) { return Launch{(void *)c->stream}; }
+
+static int use_device(lpg_ctx *c) {
+    HIPCHK(c, hipSetDevice(c->device));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// collectives: RCCL on device buffers, or caller-provided host-staged ops
+// ---------------------------------------------------------------------------
+
+static int comm_allgather(lpg_ctx *c, const void *send, void *recv, size_t bytes) {
+    if (c->world == 1) return 0;
+    if (c->nccl) {
+        ncclResult_t r = ncclAllGather(send, recv, bytes, ncclUint8, c->nccl, c->stream);
+        if (r != ncclSuccess) return fail(c, LPG_ERR_COMM, "ncclAllGather: %s", ncclGetErrorString(r));
+        return 0;
+    }
+    if (!c->have_hops) return fail(c, LPG_ERR_STATE, "world > 1 but no communicator attached");
+    c->hsend.resize(bytes);
+    c->hrecv.resize(bytes * c->world);
+    HIPCHK(c, hipMemcpyAsync(c->hsend.data(), send, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->hops.allgather(c->hops.user, c->hsend.data(), c->hrecv.data(), bytes) != 0)
+        return fail(c, LPG_ERR_COMM, "host allgather callback failed");
+    HIPCHK(c, hipMemcpyAsync(recv, c->hrecv.data(), bytes * c->world, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+static int comm_allreduce_sum(lpg_ctx *c, double *buf, size_t count) {
+    if (c->world == 1) return 0;
+    if (c->nccl) {
+        ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, c->nccl, c->stream);
+        if (r != ncclSuccess) return fail(c, LPG_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+        return 0;
+    }
+    if (!c->have_hops) return fail(c, LPG_ERR_STATE, "world > 1 but no communicator attached");
+    c->hsend.resize(count * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->hsend.data(), buf, count * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->hops.allreduce_sum_f64(c->hops.user, (double *)c->hsend.data(), count) != 0)
+        return fail(c, LPG_ERR_COMM, "host allreduce callback failed");
+    HIPCHK(c, hipMemcpyAsync(buf, c->hsend.data(), count * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// timing ring
+// ---------------------------------------------------------------------------
+
+static int timing_flush(lpg_ctx *c) {
+    TimingRing &t = c->tr;
+    if (t.used == 0) return 0;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int q = 0; q < t.used; q++) {
+        float a = 0, b = 0;
+        HIPCHK(c, hipEventElapsedTime(&a, t.ev[3 * q], t.ev[3 * q + 1]));
+        HIPCHK(c, hipEventElapsedTime(&b, t.ev[3 * q + 1], t.ev[3 * q + 2]));
+        t.select_ms += a;
+        t.update_ms += b;
+        t.count++;
+    }
+    t.used = 0;
+    return 0;
+}
+
+static int timing_mark(lpg_ctx *c, int which) {
+    TimingRing &t = c->tr;
+    if (which == 0 && t.used * 3 + 3 > (int)t.ev.size()) {
+        int rc = timing_flush(c);
+        if (rc) return rc;
+    }
+    HIPCHK(c, hipEventRecord(t.ev[3 * t.used + which], c->stream));
+    if (which == 2) t.used++;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// pivot loop
+// ---------------------------------------------------------------------------
+
+static int exchange_candidates(lpg_ctx *c) {
+    if (c->world == 1) return 0;
+    return comm_allgather(c, c->part, c->cand, sizeof(Cand) * (size_t)c->nsel);
+}
+
+static int bootstrap(lpg_ctx *c, int rule) {
+    HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
+    const Geo g = geo(c);
+    if (launch_price(lau(c), g, rule, 0, c->st, 0, c->P, c->C[0], c->pp, c->npp))
+        return fail(c, LPG_ERR_DEVICE, "price launch failed");
+    if (launch_select(lau(c), g, rule, true, c->st, 0, 0, c->P, c->C[1], c->C[0], c->pp, c->npp, c->basis,
+                      c->part, c->nsel))
+        return fail(c, LPG_ERR_DEVICE, "select launch failed");
+    int rc = exchange_candidates(c);
+    if (rc) return rc;
+    c->par = 0;
+    c->booted = true;
+    c->boot_rule = rule;
+    return 0;
+}
+
+static int enqueue(lpg_ctx *c, int64_t npiv, int rule) {
+    if (!c->booted || c->boot_rule != rule) {
+        int rc = bootstrap(c, rule);
+        if (rc) return rc;
+    }
+    const Geo g = geo(c);
+    const Launch L = lau(c);
+    const bool fuse = c->world == 1;
+    const int ncand = c->nsel * c->world;
+    for (int64_t q = 0; q < npiv; q++) {
+        const int s = c->par, s1 = s ^ 1;
+        int rc;
+        if (c->timing && (rc = timing_mark(c, 0))) return rc;
+        if (launch_prep(L, g, rule, fuse, c->st, s, c->cand, ncand, c->P, c->C[s], c->pp, c->npp))
+            return fail(c, LPG_ERR_DEVICE, "prep launch failed");
+        if (!fuse) {
+            if ((rc = comm_allreduce_sum(c, c->P, (size_t)c->ld))) return rc;
+            if (launch_price(L, g, rule, 1, c->st, s, c->P, c->C[s], c->pp, c->npp))
+                return fail(c, LPG_ERR_DEVICE, "price launch failed");
+        }
+        if (launch_select(L, g, rule, false, c->st, s, s1, c->P, c->C[s], c->C[s1], c->pp, c->npp, c->basis,
+                          c->part, c->nsel))
+            return fail(c, LPG_ERR_DEVICE, "select launch failed");
+        if ((rc = exchange_candidates(c))) return rc;
+        if (c->timing && (rc = timing_mark(c, 1))) return rc;
+        if (launch_update(L, g, c->st, s, c->P, c->C[s], c->basis, c->logk, c->logr, c->update_variant))
+            return fail(c, LPG_ERR_DEVICE, "update launch failed");
+        if (c->timing && (rc = timing_mark(c, 2))) return rc;
+        c->par = s1;
+        c->enq++;
+    }
+    return 0;
+}
+
+static int read_result(lpg_ctx *c, lpg_result *out, int rule) {
+    DevState h;
+    HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    double z = 0;
+    HIPCHK(c, hipMemcpyAsync(&z, c->T + c->nloc * c->ld, sizeof z, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (out) {
+        const int32_t s = c->booted ? h.slot[c->par].status : RUNNING;
+        out->status = s == RUNNING ? LPG_ITER_LIMIT : s;
+        out->rule = rule;
+        out->pivots = h.pivots;
+        out->objective = z;
+        out->entering = h.pivots ? h.last_k : -1;
+        out->leaving = h.pivots ? h.last_r : -1;
+    }
+    return 0;
+}
+
+static int reset_state(lpg_ctx *c) {
+    DevState h;
+    memset(&h, 0, sizeof h);
+    h.logcap = c->logcap;
+    h.last_k = h.last_r = -1;
+    HIPCHK(c, hipMemcpyAsync(c->st, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->booted = false;
+    c->par = 0;
+    c->enq = 0;
+    return 0;
+}
+
+static int ensure_log(lpg_ctx *c, int64_t need) {
+    if (c->flags & LPG_FLAG_NO_LOG) return 0;
+    if (need <= c->logcap) return 0;
+    int64_t cap = std::max<int64_t>(need, 2 * c->logcap);
+    int64_t *nk = nullptr, *nr = nullptr;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMalloc(&nk, cap * sizeof(int64_t)));
+    HIPCHK(c, hipMalloc(&nr, cap * sizeof(int64_t)));
+    if (c->logk) {
+        HIPCHK(c, hipMemcpy(nk, c->logk, c->logcap * sizeof(int64_t), hipMemcpyDeviceToDevice));
+        HIPCHK(c, hipMemcpy(nr, c->logr, c->logcap * sizeof(int64_t), hipMemcpyDeviceToDevice));
+        HIPCHK(c, hipFree(c->logk));
+        HIPCHK(c, hipFree(c->logr));
+    }
+    c->logk = nk;
+    c->logr = nr;
+    c->logcap = cap;
+    HIPCHK(c, hipMemcpy(&c->st->logcap, &cap, sizeof cap, hipMemcpyHostToDevice));
+    return 0;
+}
+
+static int64_t device_pivots(lpg_ctx *c) {
+    int64_t n = 0;
+    if (hipMemcpy(&n, &c->st->pivots, sizeof n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return n;
+}
+
+// ---------------------------------------------------------------------------
+// extern "C" API
+// ---------------------------------------------------------------------------
+
+extern "C" {
+
+const char *lpg_last_error(const lpg_ctx *c) { return c ? c->err : g_err; }
+
+int lpg_device_count(int *count) {
+    if (!count) return fail(nullptr, LPG_ERR_ARG, "count is NULL");
+    hipError_t e = hipGetDeviceCount(count);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(nullptr, LPG_ERR_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    return 0;
+}
+
+int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, int64_t ncols, uint32_t flags) {
+    if (!out) return fail(nullptr, LPG_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (m < 1 || ncols < 2 || world < 1 || rank < 0 || rank >= world || world > m)
+        return fail(nullptr, LPG_ERR_ARG, "bad shape m=%lld ncols=%lld world=%d rank=%d", (long long)m,
+                    (long long)ncols, world, rank);
+    lpg_ctx *c = new lpg_ctx();
+    c->device = device;
+    c->world = world;
+    c->rank = rank;
+    c->m = m;
+    c->ncols = ncols;
+    c->ld = (ncols + 63) & ~(int64_t)63;   // 512-byte aligned rows
+    c->row0 = m * rank / world;
+    c->nloc = m * (rank + 1) / world - c->row0;
+    c->nact = ncols - 1;
+    c->flags = flags;
+    const char *uv = getenv("LPG_UPDATE_VARIANT");
+    c->update_variant = uv ? atoi(uv) : 0;
+    int rc;
+    if ((rc = use_device(c))) { lpg_destroy(c); return rc; }
+    const int64_t rows = c->nloc + c->nobj;
+    const Geo g = geo(c);
+    c->npp = price_blocks(g);
+    const int64_t maxloc = (m + world - 1) / world + c->nobj;   // identical on every rank
+    c->nsel = (int)std::min<int64_t>((maxloc + kBlock - 1) / kBlock, kMaxSelBlocks);
+#define ALLOC(p, bytes)                                                                    \
+    do {                                                                                   \
+        hipError_t e_ = hipMalloc((void **)&(p), (bytes));                                 \
+        if (e_ != hipSuccess) {                                                            \
+            fail(c, LPG_ERR_OOM, "hipMalloc(%s, %zu): %s", #p, (size_t)(bytes), hipGetErrorString(e_)); \
+            snprintf(g_err, sizeof g_err, "%s", c->err);                                   \
+            lpg_destroy(c);                                                                \
+            return LPG_ERR_OOM;                                                            \
+        }                                                                                  \
+    } while (0)
+    ALLOC(c->T, (size_t)rows * c->ld * sizeof(double));
+    ALLOC(c->P, (size_t)c->ld * sizeof(double));
+    ALLOC(c->C[0], (size_t)rows * sizeof(double));
+    ALLOC(c->C[1], (size_t)rows * sizeof(double));
+    ALLOC(c->acc, (size_t)c->ld * world * sizeof(double));
+    ALLOC(c->cb, (size_t)std::max<int64_t>(c->nloc, 1) * sizeof(double));
+    ALLOC(c->cost, (size_t)ncols * sizeof(double));
+    ALLOC(c->pp, (size_t)c->npp * sizeof(PricePart));
+    ALLOC(c->part, (size_t)c->nsel * sizeof(Cand));
+    if (world > 1) ALLOC(c->cand, (size_t)c->nsel * world * sizeof(Cand));
+    else c->cand = c->part;
+    ALLOC(c->basis, (size_t)m * sizeof(int64_t));
+    ALLOC(c->st, sizeof(DevState));
+#undef ALLOC
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        fail(c, LPG_ERR_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+        lpg_destroy(c);
+        return LPG_ERR_DEVICE;
+    }
+    c->own_stream = true;
+    if (hipMemset(c->T, 0, (size_t)rows * c->ld * sizeof(double)) != hipSuccess ||
+        hipMemset(c->P, 0, (size_t)c->ld * sizeof(double)) != hipSuccess ||
+        hipMemset(c->basis, 0, (size_t)m * sizeof(int64_t)) != hipSuccess) {
+        fail(c, LPG_ERR_DEVICE, "hipMemset failed");
+        lpg_destroy(c);
+        return LPG_ERR_DEVICE;
+    }
+    if ((rc = ensure_log(c, 1024)) || (rc = reset_state(c))) {
+        lpg_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return 0;
+}
+
+int lpg_create(lpg_ctx **out, int device, int64_t m, int64_t ncols, uint32_t flags) {
+    return lpg_create_dist(out, device, 1, 0, m, ncols, flags);
+}
+
+int lpg_comm_unique_id(void *uid, size_t len) {
+    if (!uid || len < sizeof(ncclUniqueId)) return fail(nullptr, LPG_ERR_ARG, "uid buffer too small");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(nullptr, LPG_ERR_COMM, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+    memcpy(uid, &id, sizeof id);
+    return 0;
+}
+
+int lpg_comm_init_rccl(lpg_ctx *c, const void *uid, size_t len) {
+    if (!c || !uid || len < sizeof(ncclUniqueId)) return fail(c, LPG_ERR_ARG, "bad uid");
+    if (c->world == 1) return 0;
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    ncclUniqueId id;
+    memcpy(&id, uid, sizeof id);
+    ncclResult_t r = ncclCommInitRank(&c->nccl, c->world, id, c->rank);
+    if (r != ncclSuccess) {
+        c->nccl = nullptr;
+        return fail(c, LPG_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    return 0;
+}
+
+int lpg_comm_init_host(lpg_ctx *c, const lpg_host_comm_ops *ops) {
+    if (!c || !ops || !ops->allgather || !ops->allreduce_sum_f64) return fail(c, LPG_ERR_ARG, "bad host comm ops");
+    c->hops = *ops;
+    c->have_hops = true;
+    return 0;
+}
+
+void lpg_destroy(lpg_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->nccl) ncclCommDestroy(c->nccl);
+    for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
+    if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
+    void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->part, c->basis, c->logk, c->logr, c->st};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int lpg_info(const lpg_ctx *c, lpg_info_t *o) {
+    if (!c || !o) return fail(const_cast<lpg_ctx *>(c), LPG_ERR_ARG, "NULL argument");
+    o->m = c->m;
+    o->ncols = c->ncols;
+    o->ld = c->ld;
+    o->row0 = c->row0;
+    o->nrows = c->nloc;
+    o->world = c->world;
+    o->rank = c->rank;
+    o->device = c->device;
+    o->nobj = (int32_t)c->nobj;
+    o->bytes_per_pivot = 16.0 * (double)(c->nloc + c->nobj) * (double)c->ncols;
+    return 0;
+}
+
+int lpg_load_rows(lpg_ctx *c, int64_t row0, int64_t nrows, const double *rows, int64_t ld) {
+    if (!c || !rows || row0 < 0 || nrows < 0 || row0 + nrows > c->m + c->nobj || ld < c->ncols)
+        return fail(c, LPG_ERR_ARG, "lpg_load_rows: bad arguments");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    // constraint rows inside this rank's block
+    const int64_t a = std::max(row0, c->row0), b = std::min(row0 + nrows, c->row0 + c->nloc);
+    if (a < b)
+        HIPCHK(c, hipMemcpy2D(c->T + (a - c->row0) * c->ld, c->ld * sizeof(double), rows + (a - row0) * ld,
+                              ld * sizeof(double), c->ncols * sizeof(double), b - a, hipMemcpyHostToDevice));
+    // objective row(s): global index m + q, replicated on every rank
+    for (int64_t q = 0; q < c->nobj; q++) {
+        const int64_t gi = c->m + q;
+        if (gi >= row0 && gi < row0 + nrows)
+            HIPCHK(c, hipMemcpy(c->T + (c->nloc + q) * c->ld, rows + (gi - row0) * ld, c->ncols * sizeof(double),
+                                hipMemcpyHostToDevice));
+    }
+    return reset_state(c);
+}
+
+int lpg_set_basis(lpg_ctx *c, const int64_t *basis) {
+    if (!c || !basis) return fail(c, LPG_ERR_ARG, "basis is NULL");
+    for (int64_t i = 0; i < c->m; i++)
+        if (basis[i] < 1 || basis[i] >= c->ncols) return fail(c, LPG_ERR_ARG, "basis[%lld] out of range", (long long)i);
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    HIPCHK(c, hipMemcpy(c->basis, basis, c->m * sizeof(int64_t), hipMemcpyHostToDevice));
+    return reset_state(c);
+}
+
+int lpg_set_objective(lpg_ctx *c, const double *cost) {
+    if (!c || !cost) return fail(c, LPG_ERR_ARG, "cost is NULL");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    std::vector<int64_t> hb(c->m);
+    HIPCHK(c, hipMemcpy(hb.data(), c->basis, c->m * sizeof(int64_t), hipMemcpyDeviceToHost));
+    std::vector<double> hcb(std::max<int64_t>(c->nloc, 1));
+    for (int64_t i = 0; i < c->nloc; i++) {
+        const int64_t col = hb[c->row0 + i];
+        if (col < 1 || col >= c->ncols) return fail(c, LPG_ERR_STATE, "basis not set (row %lld)", (long long)(c->row0 + i));
+        hcb[i] = cost[col - 1];
+    }
+    HIPCHK(c, hipMemcpy(c->cb, hcb.data(), c->nloc * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->cost, cost, (c->ncols - 1) * sizeof(double), hipMemcpyHostToDevice));
+    const Geo g = geo(c);
+    // Chain the fma sum over ranks in global row order: round p, rank p
+    // extends the chain; everybody receives it through a sum with zeros.
+    double *chain = c->acc;
+    for (int p = 0; p < c->world; p++) {
+        if (c->rank == p) {
+            if (launch_objective_chain(lau(c), g, c->cb, p == 0 ? nullptr : chain, chain))
+                return fail(c, LPG_ERR_DEVICE, "objective chain launch failed");
+        } else {
+            HIPCHK(c, hipMemsetAsync(chain, 0, c->ncols * sizeof(double), c->stream));
+        }
+        if ((rc = comm_allreduce_sum(c, chain, (size_t)c->ncols))) return rc;
+    }
+    if (launch_objective_finish(lau(c), g, chain, c->cost)) return fail(c, LPG_ERR_DEVICE, "objective finish failed");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return reset_state(c);
+}
+
+int lpg_set_tolerances(lpg_ctx *c, double eps_piv, double eps_opt) {
+    if (!c || !(eps_piv >= 0) || !(eps_opt >= 0)) return fail(c, LPG_ERR_ARG, "bad tolerances");
+    c->eps_piv = eps_piv;
+    c->eps_opt = eps_opt;
+    c->booted = false;
+    return 0;
+}
+
+int lpg_set_active_columns(lpg_ctx *c, int64_t nact) {
+    if (!c || nact < 1 || nact > c->ncols - 1) return fail(c, LPG_ERR_ARG, "bad active column count");
+    c->nact = nact;
+    c->booted = false;
+    return 0;
+}
+
+int lpg_generate(lpg_ctx *c, int64_t n, uint64_t seed, int kind) {
+    if (!c || n < 1 || c->ncols != n + c->m + 1 || (kind != LPG_GEN_DENSE && kind != LPG_GEN_DEGENERATE))
+        return fail(c, LPG_ERR_ARG, "lpg_generate: need ncols == n + m + 1 and a known kind");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    if (launch_generate(lau(c), geo(c), n, seed, kind, c->basis)) return fail(c, LPG_ERR_DEVICE, "generate launch failed");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return reset_state(c);
+}
+
+int lpg_enqueue(lpg_ctx *c, int64_t npiv, int rule) {
+    if (!c || npiv < 0 || (rule != LPG_RULE_DANTZIG && rule != LPG_RULE_BLAND))
+        return fail(c, LPG_ERR_ARG, "lpg_enqueue: bad arguments");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    if ((rc = ensure_log(c, c->enq + npiv))) return rc;
+    return enqueue(c, npiv, rule);
+}
+
+int lpg_reserve_log(lpg_ctx *c, int64_t npivots) {
+    if (!c || npivots < 0) return fail(c, LPG_ERR_ARG, "lpg_reserve_log: bad arguments");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    return ensure_log(c, c->enq + npivots);
+}
+
+int lpg_sync(lpg_ctx *c, lpg_result *out) {
+    if (!c) return fail(c, LPG_ERR_ARG, "ctx is NULL");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    return read_result(c, out, c->boot_rule);
+}
+
+int lpg_solve(lpg_ctx *c, int64_t max_pivots, int rule, lpg_result *out) {
+    if (!c || max_pivots < 0 || (rule != LPG_RULE_DANTZIG && rule != LPG_RULE_BLAND))
+        return fail(c, LPG_ERR_ARG, "lpg_solve: bad arguments");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    lpg_result r;
+    if (c->booted && c->boot_rule == rule) {
+        if ((rc = read_result(c, &r, rule))) return rc;
+        if (r.status != LPG_ITER_LIMIT) {
+            if (out) *out = r;
+            return 0;
+        }
+    }
+    int64_t done = 0, batch = 8;
+    if (max_pivots == 0) {
+        if (!c->booted || c->boot_rule != rule)
+            if ((rc = enqueue(c, 0, rule))) return rc;
+    }
+    while (done < max_pivots) {
+        const int64_t n = std::min(batch, max_pivots - done);
+        if ((rc = lpg_enqueue(c, n, rule))) return rc;
+        done += n;
+        if ((rc = read_result(c, &r, rule))) return rc;
+        if (r.status != LPG_ITER_LIMIT) break;
+        batch = std::min<int64_t>(batch * 2, 256);
+    }
+    return read_result(c, out, rule);
+}
+
+int lpg_get_rows(lpg_ctx *c, int64_t row0, int64_t nrows, double *out, int64_t ld) {
+    if (!c || !out || row0 < 0 || nrows < 0 || row0 + nrows > c->m + c->nobj || ld < c->ncols)
+        return fail(c, LPG_ERR_ARG, "lpg_get_rows: bad arguments");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int64_t a = std::max(row0, c->row0), b = std::min(row0 + nrows, c->row0 + c->nloc);
+    if (a < b)
+        HIPCHK(c, hipMemcpy2D(out + (a - row0) * ld, ld * sizeof(double), c->T + (a - c->row0) * c->ld,
+                              c->ld * sizeof(double), c->ncols * sizeof(double), b - a, hipMemcpyDeviceToHost));
+    for (int64_t q = 0; q < c->nobj; q++) {
+        const int64_t gi = c->m + q;
+        if (gi >= row0 && gi < row0 + nrows)
+            HIPCHK(c, hipMemcpy(out + (gi - row0) * ld, c->T + (c->nloc + q) * c->ld, c->ncols * sizeof(double),
+                                hipMemcpyDeviceToHost));
+    }
+    return 0;
+}
+
+int lpg_get_basis(lpg_ctx *c, int64_t *basis) {
+    if (!c || !basis) return fail(c, LPG_ERR_ARG, "basis is NULL");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(basis, c->basis, c->m * sizeof(int64_t), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int lpg_get_column0(lpg_ctx *c, double *xB) {
+    if (!c || !xB) return fail(c, LPG_ERR_ARG, "xB is NULL");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->nloc)
+        HIPCHK(c, hipMemcpy2D(xB, sizeof(double), c->T, c->ld * sizeof(double), sizeof(double), c->nloc,
+                              hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int64_t lpg_get_log(lpg_ctx *c, int64_t *k, int64_t *r, int64_t max) {
+    if (!c || max < 0) return fail(c, LPG_ERR_ARG, "lpg_get_log: bad arguments");
+    if (use_device(c)) return LPG_ERR_DEVICE;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(c, LPG_ERR_DEVICE, "sync failed");
+    const int64_t n = device_pivots(c);
+    if (n < 0) return fail(c, LPG_ERR_DEVICE, "reading pivot count failed");
+    if (c->flags & LPG_FLAG_NO_LOG) return n;
+    const int64_t cnt = std::min(std::min(n, max), c->logcap);
+    if (cnt > 0) {
+        if (k && hipMemcpy(k, c->logk, cnt * sizeof(int64_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(c, LPG_ERR_DEVICE, "log copy failed");
+        if (r && hipMemcpy(r, c->logr, cnt * sizeof(int64_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(c, LPG_ERR_DEVICE, "log copy failed");
+    }
+    return n;
+}
+
+int lpg_set_timing(lpg_ctx *c, int enable) {
+    if (!c) return fail(c, LPG_ERR_ARG, "ctx is NULL");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    if (enable && c->tr.ev.empty()) {
+        c->tr.ev.resize(3 * 1024);
+        for (auto &e : c->tr.ev) HIPCHK(c, hipEventCreate(&e));
+    }
+    c->timing = enable != 0;
+    return 0;
+}
+
+int lpg_get_timing(lpg_ctx *c, lpg_timing *out) {
+    if (!c || !out) return fail(c, LPG_ERR_ARG, "NULL argument");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    if ((rc = timing_flush(c))) return rc;
+    out->update_ms = c->tr.update_ms;
+    out->select_ms = c->tr.select_ms;
+    out->comm_ms = c->tr.comm_ms;
+    out->update_count = c->tr.count;
+    c->tr.update_ms = c->tr.select_ms = c->tr.comm_ms = 0;
+    c->tr.count = 0;
+    return 0;
+}
+
+int lpg_device_sync(lpg_ctx *c) {
+    if (!c) return fail(c, LPG_ERR_ARG, "ctx is NULL");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+// lpg_internal.h — device-side data structures shared by the kernels
+// (lpg_kernels.hip) and the context / C-ABI layer (lpg_ctx.hip).
+//
+// Per pivot t the device keeps everything the host would otherwise have to
+// read back, so the host enqueues pivots without synchronising:
+//   slot[t & 1]   entering column k_t (chosen by select_{t-1}), leaving row
+//                 r_t (chosen by prep_t from the gathered ratio candidates),
+//                 and a status that, once non-RUNNING, turns every later
+//                 kernel into a no-op and is copied forward slot to slot.
+//   C[t & 1]      column k_t of T_t (the pivot-column snapshot), written by
+//                 select_{t-1} and read by update_t.
+//   P             the normalised pivot row of T_t, written by prep_t.
+#pragma once
+#include <stdint.h>
+
+namespace lpg {
+
+constexpr int kBlock = 256;          // threads per block everywhere (4 waves of 64)
+constexpr int kMaxSelBlocks = 512;   // ratio-test partials per rank
+
+enum : int32_t { RUNNING = 0, OPTIMAL = 1, UNBOUNDED = 2, INFEASIBLE = 3, ITER_LIMIT = 4, NUMERIC = 5 };
+enum : int { RULE_DANTZIG = 0, RULE_BLAND = 1 };
+
+struct Slot {                 // 32 B
+    int64_t k;                // entering column (1-based)
+    int64_t r;                // leaving row (global)
+    int32_t status;
+    int32_t pad0;
+    int64_t pad1;
+};
+
+struct DevState {
+    Slot    slot[2];
+    int64_t pivots;           // pivots applied (update kernels that ran)
+    int64_t last_k, last_r;
+    int64_t logcap;
+};
+
+// Ratio-test candidate: lexicographic (theta, key); row < 0 = none.
+struct Cand {                 // 32 B
+    double  theta;
+    double  piv;              // the pivot element T_t[row][k_t] (replicated check)
+    int64_t key;              // row (Dantzig) or basic column (Bland)
+    int64_t row;              // global row
+};
+
+// Pricing partial: Dantzig (v, j) lexicographic; Bland smallest eligible j.
+struct PricePart {            // 16 B
+    double  v;
+    int64_t j;                // -1 = none
+};
+
+// Geometry of this rank's slice of the tableau.
+struct Geo {
+    double *T;                // (nloc + nobj) x ld, row-major; objective row(s) last
+    int64_t ld;               // row pitch in doubles (multiple of 64)
+    int64_t nloc;             // local constraint rows
+    int64_t nobj;             // objective rows (1)
+    int64_t ncols;            // N + 1
+    int64_t nact;             // price columns 1..nact
+    int64_t row0;             // global index of local row 0
+    int64_t m;                // global constraint rows
+    double  eps_piv, eps_opt;
+};
+
+// ---- launchers (lpg_kernels.hip) ----
+struct Launch {
+    void   *stream;           // hipStream_t
+};
+
+int launch_generate(const Launch &L, const Geo &g, int64_t n, uint64_t seed, int kind, int64_t *basis_dev);
+int launch_objective_chain(const Launch &L, const Geo &g, const double *cb, const double *acc_in, double *acc_out);
+int launch_objective_finish(const Launch &L, const Geo &g, const double *acc, const double *cost);
+int launch_price(const Launch &L, const Geo &g, int rule, int mode, const DevState *st, int s,
+                 const double *P, const double *Cs, PricePart *pp, int npp);
+int launch_prep(const Launch &L, const Geo &g, int rule, bool fuse_price, DevState *st, int s,
+                const Cand *cand, int ncand, double *P, const double *Cs, PricePart *pp, int npp);
+int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState *st, int s, int s1,
+                  const double *P, const double *Cs, double *Cs1, const PricePart *pp, int npp,
+                  const int64_t *basis, Cand *part, int nsel);
+int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
+                  int64_t *basis, int64_t *logk, int64_t *logr, int variant);
+
+int price_blocks(const Geo &g);      // number of pricing partials (= prep / price grid)
+
+}  // namespace lpg

@@ -1,0 +1,597 @@
+// lpg_kernels.hip — gfx950 kernels of the dense-tableau simplex pivot engine.
+//
+// One pivot t = prep_t -> select_t -> update_t on one stream (plus, with
+// world > 1, an allreduce of P after prep and an allgather of the ratio
+// candidates after select). The arithmetic is the bitwise contract of
+// oracle/lpo.h (built with -ffp-contract=off; every fused multiply-add below
+// is an explicit fma):
+//   P[j]    = T[r][j] / T[r][k]
+//   T[i][j] = fma(-C[i], P[j], T[i][j])   for i != r,   T[r][j] = P[j]
+// Reference anchors: the loop these kernels implement is absent upstream
+// (Source/simplex.c:40 -> :65); the tableau they run on is SimplexMatrix
+// (Source/matrix.h:13-21) with column 0 = b (Source/matrix.c:42-48).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "lpg_internal.h"
+
+namespace lpg {
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+// ------------------------------------------------------------------------
+// reductions: 64-lane wave shuffles, then the 4 waves through LDS
+// ------------------------------------------------------------------------
+
+__device__ __forceinline__ bool cand_better(const Cand &a, const Cand &b) {
+    if (a.row < 0) return false;
+    if (b.row < 0) return true;
+    if (a.theta != b.theta) return a.theta < b.theta;
+    return a.key < b.key;
+}
+
+template <int RULE>
+__device__ __forceinline__ bool pp_better(const PricePart &a, const PricePart &b) {
+    if (a.j < 0) return false;
+    if (b.j < 0) return true;
+    if (RULE == RULE_BLAND) return a.j < b.j;
+    if (a.v != b.v) return a.v < b.v;
+    return a.j < b.j;
+}
+
+__device__ __forceinline__ Cand shfl_xor_cand(const Cand &c, int mask) {
+    Cand o;
+    o.theta = __shfl_xor(c.theta, mask, 64);
+    o.piv = __shfl_xor(c.piv, mask, 64);
+    o.key = __shfl_xor((long long)c.key, mask, 64);
+    o.row = __shfl_xor((long long)c.row, mask, 64);
+    return o;
+}
+
+__device__ __forceinline__ PricePart shfl_xor_pp(const PricePart &p, int mask) {
+    PricePart o;
+    o.v = __shfl_xor(p.v, mask, 64);
+    o.j = __shfl_xor((long long)p.j, mask, 64);
+    return o;
+}
+
+// Block-wide min of a Cand; result valid in every thread.
+__device__ Cand block_reduce_cand(Cand c) {
+    __shared__ Cand sh[kBlock / 64];
+#pragma unroll
+    for (int mask = 32; mask > 0; mask >>= 1) {
+        Cand o = shfl_xor_cand(c, mask);
+        if (cand_better(o, c)) c = o;
+    }
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = c;
+    __syncthreads();
+    Cand b = sh[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / 64; i++)
+        if (cand_better(sh[i], b)) b = sh[i];
+    return b;
+}
+
+template <int RULE>
+__device__ PricePart block_reduce_pp(PricePart p) {
+    __shared__ PricePart sh[kBlock / 64];
+#pragma unroll
+    for (int mask = 32; mask > 0; mask >>= 1) {
+        PricePart o = shfl_xor_pp(p, mask);
+        if (pp_better<RULE>(o, p)) p = o;
+    }
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = p;
+    __syncthreads();
+    PricePart b = sh[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / 64; i++)
+        if (pp_better<RULE>(sh[i], b)) b = sh[i];
+    return b;
+}
+
+// Pricing candidate of one reduced cost d_j.
+template <int RULE>
+__device__ __forceinline__ void price_one(PricePart &best, double d, int64_t j, const Geo &g) {
+    if (j < 1 || j > g.nact) return;
+    PricePart c;
+    c.v = d;
+    c.j = j;
+    if (RULE == RULE_BLAND) {
+        if (!(d < -g.eps_opt)) return;
+    } else {
+        if (!(d == d)) return;   // NaN never wins
+    }
+    if (pp_better<RULE>(c, best)) best = c;
+}
+
+// ------------------------------------------------------------------------
+// synthetic generator (bitwise identical to oracle lpo_generate)
+// ------------------------------------------------------------------------
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ double uniform01(uint64_t key, uint64_t idx) {
+    return (double)(splitmix64(key ^ (idx * 0x9E3779B97F4A7C15ull)) >> 11) * 0x1.0p-53;
+}
+
+static inline uint64_t splitmix64_host(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static inline uint64_t subkey(uint64_t seed, uint64_t which) {
+    return splitmix64_host(seed ^ (which * 0xD1B54A32D192ED03ull));
+}
+
+// grid: x = local row, y = chunk of 512 columns (256 lanes x 2). Every rank
+// fills all m basis entries (slack basis) through k_basis_slack.
+__global__ __launch_bounds__(kBlock) void k_generate(double *__restrict__ T, Geo g, int64_t n, uint64_t kA,
+                                                     uint64_t kB, uint64_t kC, int kind) {
+    const int64_t i = blockIdx.x;
+    const int64_t j0 = ((int64_t)blockIdx.y * kBlock + threadIdx.x) * 2;
+    if (j0 >= g.ld) return;
+    double *row = T + i * g.ld;
+    const double bscale = (double)n / 8.0;
+    double v[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const int64_t j = j0 + e;
+        double x = 0.0;
+        if (i < g.nloc) {
+            const int64_t gi = g.row0 + i;
+            if (j == 0) {
+                if (kind == 0 || (gi & 1))
+                    x = bscale * (1.0 + uniform01(kB, (uint64_t)gi));
+            } else if (j <= n) {
+                const int64_t jj = j - 1;
+                if (kind == 0) {
+                    x = uniform01(kA, (uint64_t)(gi * n + jj));
+                } else {
+                    if (jj < gi) x = 2.0 * uniform01(kA, (uint64_t)(gi * n + jj));
+                    else if (jj == gi) x = 1.0;
+                }
+            } else if (j == 1 + n + gi) {
+                x = 1.0;
+            }
+        } else if (i == g.nloc) {
+            if (j >= 1 && j <= n) x = -(1.0 + uniform01(kC, (uint64_t)(j - 1)));
+        }
+        v[e] = x;
+    }
+    *(d2 *)(row + j0) = d2{v[0], v[1]};
+}
+
+__global__ void k_basis_slack(int64_t *__restrict__ basis, int64_t m, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < m) basis[i] = 1 + n + i;
+}
+
+int launch_generate(const Launch &L, const Geo &g, int64_t n, uint64_t seed, int kind, int64_t *basis_dev) {
+    hipStream_t st = (hipStream_t)L.stream;
+    const int64_t rows = g.nloc + g.nobj;
+    const int64_t chunks = (g.ld / 2 + kBlock - 1) / kBlock;
+    if (rows > 0x7fffffff || chunks > 65535) return -1;
+    dim3 grid((unsigned)rows, (unsigned)chunks);
+    hipLaunchKernelGGL(k_generate, grid, dim3(kBlock), 0, st, g.T, g, n, subkey(seed, 1), subkey(seed, 2),
+                       subkey(seed, 3), kind);
+    hipLaunchKernelGGL(k_basis_slack, dim3((unsigned)((g.m + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       basis_dev, g.m, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------
+// objective row from costs: d_j = sum_i cB_i T[i][j] - c_j, chained across
+// ranks in global row order (acc_in = previous rank's partial chain)
+// ------------------------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void k_objective_chain(const double *__restrict__ T, Geo g,
+                                                            const double *__restrict__ cb,
+                                                            const double *__restrict__ acc_in,
+                                                            double *__restrict__ acc_out) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= g.ncols) return;
+    double acc = acc_in ? acc_in[j] : 0.0;
+    for (int64_t i = 0; i < g.nloc; i++) acc = fma(cb[i], T[i * g.ld + j], acc);
+    acc_out[j] = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void k_objective_finish(double *__restrict__ T, Geo g,
+                                                             const double *__restrict__ acc,
+                                                             const double *__restrict__ cost) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= g.ld) return;
+    double *obj = T + g.nloc * g.ld;
+    obj[j] = j == 0 ? acc[0] : (j < g.ncols ? acc[j] - cost[j - 1] : 0.0);
+}
+
+int launch_objective_chain(const Launch &L, const Geo &g, const double *cb, const double *acc_in,
+                           double *acc_out) {
+    hipLaunchKernelGGL(k_objective_chain, dim3((unsigned)((g.ncols + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)L.stream, g.T, g, cb, acc_in, acc_out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_objective_finish(const Launch &L, const Geo &g, const double *acc, const double *cost) {
+    hipLaunchKernelGGL(k_objective_finish, dim3((unsigned)((g.ld + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)L.stream, g.T, g, acc, cost);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------
+// pricing (a10). mode 0: price the objective row as stored (bootstrap);
+// mode 1: price d_{t+1} = fma(-C_t[obj], P_t[j], d_t[j]) before the update
+// writes it (multi-GPU path, after the allreduce of P).
+// ------------------------------------------------------------------------
+
+int price_blocks(const Geo &g) {
+    const int64_t nvec = (g.ncols + 1) / 2;
+    return (int)((nvec + kBlock - 1) / kBlock);
+}
+
+template <int RULE, int MODE>
+__global__ __launch_bounds__(kBlock) void k_price(const double *__restrict__ T, Geo g,
+                                                  const DevState *__restrict__ st, int s,
+                                                  const double *__restrict__ P, const double *__restrict__ Cs,
+                                                  PricePart *__restrict__ pp) {
+    if (MODE == 1 && st->slot[s].status != RUNNING) return;
+    const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t nvec = (g.ncols + 1) / 2;
+    PricePart best{0.0, -1};
+    if (j2 < nvec) {
+        const d2 d = *(const d2 *)(T + g.nloc * g.ld + 2 * j2);
+        d2 dn = d;
+        if (MODE == 1) {
+            const double c = -Cs[g.nloc];
+            const d2 p = *(const d2 *)(P + 2 * j2);
+            dn.x = fma(c, p.x, d.x);
+            dn.y = fma(c, p.y, d.y);
+        }
+        price_one<RULE>(best, dn.x, 2 * j2, g);
+        price_one<RULE>(best, dn.y, 2 * j2 + 1, g);
+    }
+    best = block_reduce_pp<RULE>(best);
+    if (threadIdx.x == 0) pp[blockIdx.x] = best;
+}
+
+int launch_price(const Launch &L, const Geo &g, int rule, int mode, const DevState *st, int s,
+                 const double *P, const double *Cs, PricePart *pp, int npp) {
+    hipStream_t stream = (hipStream_t)L.stream;
+    dim3 grid(npp), blk(kBlock);
+    if (rule == RULE_BLAND) {
+        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_BLAND, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp);
+        else hipLaunchKernelGGL((k_price<RULE_BLAND, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp);
+    } else {
+        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_DANTZIG, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp);
+        else hipLaunchKernelGGL((k_price<RULE_DANTZIG, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------
+// prep_t: leaving row from the gathered ratio candidates, normalised pivot
+// row P (owner rank; zeros elsewhere), and — single rank — the pricing of
+// d_{t+1} fused in (it only needs P and the objective row).
+// ------------------------------------------------------------------------
+
+template <int RULE, bool FUSE>
+__global__ __launch_bounds__(kBlock) void k_prep(const double *__restrict__ T, Geo g, DevState *st, int s,
+                                                 const Cand *__restrict__ cand, int ncand,
+                                                 double *__restrict__ P, const double *__restrict__ Cs,
+                                                 PricePart *__restrict__ pp) {
+    if (st->slot[s].status != RUNNING) return;
+    Cand best{0.0, 0.0, 0, -1};
+    for (int q = threadIdx.x; q < ncand; q += kBlock) {
+        const Cand c = cand[q];
+        if (cand_better(c, best)) best = c;
+    }
+    best = block_reduce_cand(best);
+    if (best.row < 0 || !isfinite(best.piv) || !isfinite(best.theta)) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->slot[s].status = best.row < 0 ? UNBOUNDED : NUMERIC;
+            st->slot[s].r = -1;
+        }
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->slot[s].r = best.row;
+    const int64_t rl = best.row - g.row0;
+    const bool own = rl >= 0 && rl < g.nloc;
+    const double piv = best.piv;   // == T_t[r][k_t] (select_{t-1} computed and stored it)
+
+    const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t nvec = (g.ncols + 1) / 2;
+    PricePart pbest{0.0, -1};
+    if (j2 < nvec) {
+        d2 p = d2{0.0, 0.0};
+        if (own) {
+            const d2 t = *(const d2 *)(T + rl * g.ld + 2 * j2);
+            p.x = t.x / piv;
+            p.y = t.y / piv;
+        }
+        *(d2 *)(P + 2 * j2) = p;
+        if (FUSE) {
+            const d2 d = *(const d2 *)(T + g.nloc * g.ld + 2 * j2);
+            const double c = -Cs[g.nloc];
+            price_one<RULE>(pbest, fma(c, p.x, d.x), 2 * j2, g);
+            price_one<RULE>(pbest, fma(c, p.y, d.y), 2 * j2 + 1, g);
+        }
+    }
+    if (FUSE) {
+        pbest = block_reduce_pp<RULE>(pbest);
+        if (threadIdx.x == 0) pp[blockIdx.x] = pbest;
+    }
+}
+
+int launch_prep(const Launch &L, const Geo &g, int rule, bool fuse, DevState *st, int s, const Cand *cand,
+                int ncand, double *P, const double *Cs, PricePart *pp, int npp) {
+    hipStream_t stream = (hipStream_t)L.stream;
+    dim3 grid(npp), blk(kBlock);
+    if (rule == RULE_BLAND) {
+        if (fuse) hipLaunchKernelGGL((k_prep<RULE_BLAND, true>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp);
+        else hipLaunchKernelGGL((k_prep<RULE_BLAND, false>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp);
+    } else {
+        if (fuse) hipLaunchKernelGGL((k_prep<RULE_DANTZIG, true>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp);
+        else hipLaunchKernelGGL((k_prep<RULE_DANTZIG, false>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------
+// select_t (a10 finish + a11): entering column k_{t+1} from the pricing
+// partials, then the ratio test on T_{t+1}'s columns 0 and k_{t+1}, computed
+// from T_t with the same fma the update will apply (the update runs after
+// this kernel, so T still holds T_t). Also stores C_{t+1} = T_{t+1}[:, k].
+// FIRST: bootstrap on the tableau as loaded (no pending pivot).
+// ------------------------------------------------------------------------
+
+template <int RULE, bool FIRST>
+__global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T, Geo g, DevState *st, int s,
+                                                   int s1, const double *__restrict__ P,
+                                                   const double *__restrict__ Cs, double *__restrict__ Cs1,
+                                                   const PricePart *__restrict__ pp, int npp,
+                                                   const int64_t *__restrict__ basis, Cand *__restrict__ part) {
+    Slot *dst = &st->slot[s1];
+    if (!FIRST) {
+        const int32_t stt = st->slot[s].status;
+        if (stt != RUNNING) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                dst->status = stt;
+                dst->k = -1;
+                dst->r = -1;
+            }
+            return;
+        }
+    }
+    PricePart pb{0.0, -1};
+    for (int q = threadIdx.x; q < npp; q += kBlock) {
+        const PricePart c = pp[q];
+        if (pp_better<RULE>(c, pb)) pb = c;
+    }
+    pb = block_reduce_pp<RULE>(pb);
+    const bool optimal = pb.j < 0 || (RULE == RULE_DANTZIG && !(pb.v < -g.eps_opt));
+    if (optimal) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            dst->status = OPTIMAL;
+            dst->k = -1;
+            dst->r = -1;
+        }
+        return;
+    }
+    const int64_t kn = pb.j;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        dst->status = RUNNING;
+        dst->k = kn;
+    }
+    int64_t rl = -1, kc = 0, r = -1;
+    double p0 = 0.0, pk = 0.0;
+    if (!FIRST) {
+        r = st->slot[s].r;
+        kc = st->slot[s].k;
+        rl = r - g.row0;
+        p0 = P[0];
+        pk = P[kn];
+    }
+    const int64_t nrows = g.nloc + g.nobj;
+    Cand best{0.0, 0.0, 0, -1};
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock) {
+        const double ob = T[i * g.ld];
+        const double oa = T[i * g.ld + kn];
+        double b, a;
+        if (FIRST) {
+            b = ob;
+            a = oa;
+        } else if (i == rl) {
+            b = p0;
+            a = pk;
+        } else {
+            const double c = -Cs[i];
+            b = fma(c, p0, ob);
+            a = fma(c, pk, oa);
+        }
+        Cs1[i] = a;
+        if (i < g.nloc && a > g.eps_piv) {
+            const int64_t grow = g.row0 + i;
+            Cand c;
+            c.theta = b > 0.0 ? b / a : 0.0;
+            c.piv = a;
+            c.row = grow;
+            c.key = RULE == RULE_BLAND ? (grow == r ? kc : basis[grow]) : grow;
+            if (cand_better(c, best)) best = c;
+        }
+    }
+    best = block_reduce_cand(best);
+    if (threadIdx.x == 0) part[blockIdx.x] = best;
+}
+
+int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState *st, int s, int s1, const double *P,
+                  const double *Cs, double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part,
+                  int nsel) {
+    hipStream_t stream = (hipStream_t)L.stream;
+    dim3 grid(nsel), blk(kBlock);
+#define LPG_SEL(R, F) \
+    hipLaunchKernelGGL((k_select<R, F>), grid, blk, 0, stream, g.T, g, st, s, s1, P, Cs, Cs1, pp, npp, basis, part)
+    if (rule == RULE_BLAND) {
+        if (first) LPG_SEL(RULE_BLAND, true); else LPG_SEL(RULE_BLAND, false);
+    } else {
+        if (first) LPG_SEL(RULE_DANTZIG, true); else LPG_SEL(RULE_DANTZIG, false);
+    }
+#undef LPG_SEL
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------
+// update_t (a12): Gauss-Jordan rank-1 elimination, the HBM-bound hot loop.
+//
+// Block = 256 lanes x VPT 16-byte column slices (a 4*VPT KB column tile);
+// it walks a strip of SR rows. Each lane keeps its slice of the normalised
+// pivot row P in VGPRs for the whole strip (the register form of staging the
+// pivot row on chip: no lane ever needs another lane's P, so LDS would only
+// add a round trip). The per-row multiplier C[i] is wave-uniform and comes
+// through the scalar cache. RU rows are loaded before any is stored, so each
+// lane keeps RU*VPT 16-byte loads in flight.
+// ------------------------------------------------------------------------
+
+template <int VPT, int RU, bool NT>
+__global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g, DevState *__restrict__ st, int s,
+                                                   const double *__restrict__ P, const double *__restrict__ Cs,
+                                                   int64_t ntiles, int64_t strip_rows,
+                                                   int64_t *__restrict__ basis, int64_t *__restrict__ logk,
+                                                   int64_t *__restrict__ logr) {
+    const int32_t status = st->slot[s].status;
+    if (status != RUNNING) return;
+    const int64_t rglob = st->slot[s].r;
+    const int64_t rl = rglob - g.row0;
+    const int64_t bid = blockIdx.x;
+    const int64_t tile = bid % ntiles;
+    const int64_t strip = bid / ntiles;
+    const int64_t nrows = g.nloc + g.nobj;
+    const int64_t i0 = strip * strip_rows;
+    const int64_t i1 = i0 + strip_rows < nrows ? i0 + strip_rows : nrows;
+    const int64_t nvec = (g.ncols + 1) / 2;
+    const int64_t cb = tile * (kBlock * VPT) + threadIdx.x;
+    const int64_t ld2 = g.ld / 2;
+    d2 *__restrict__ Tv = (d2 *)T;
+    const d2 *__restrict__ Pv = (const d2 *)P;
+
+    d2 p[VPT];
+    bool ok[VPT];
+#pragma unroll
+    for (int v = 0; v < VPT; v++) {
+        ok[v] = cb + v * kBlock < nvec;
+        p[v] = ok[v] ? Pv[cb + v * kBlock] : d2{0.0, 0.0};
+    }
+
+    int64_t i = i0;
+    for (; i + RU <= i1; i += RU) {
+        d2 t[RU][VPT];
+#pragma unroll
+        for (int u = 0; u < RU; u++)
+#pragma unroll
+            for (int v = 0; v < VPT; v++)
+                if (ok[v]) {
+                    d2 *a = Tv + (i + u) * ld2 + cb + v * kBlock;
+                    t[u][v] = NT ? __builtin_nontemporal_load(a) : *a;
+                }
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+            const double c = -Cs[i + u];
+            const bool isr = (i + u) == rl;
+#pragma unroll
+            for (int v = 0; v < VPT; v++) {
+                d2 x;
+                x.x = fma(c, p[v].x, t[u][v].x);
+                x.y = fma(c, p[v].y, t[u][v].y);
+                t[u][v] = isr ? p[v] : x;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < RU; u++)
+#pragma unroll
+            for (int v = 0; v < VPT; v++)
+                if (ok[v]) {
+                    d2 *a = Tv + (i + u) * ld2 + cb + v * kBlock;
+                    if (NT) __builtin_nontemporal_store(t[u][v], a);
+                    else *a = t[u][v];
+                }
+    }
+    for (; i < i1; i++) {
+        const double c = -Cs[i];
+        const bool isr = i == rl;
+#pragma unroll
+        for (int v = 0; v < VPT; v++)
+            if (ok[v]) {
+                d2 *a = Tv + i * ld2 + cb + v * kBlock;
+                const d2 t = *a;
+                d2 x;
+                x.x = fma(c, p[v].x, t.x);
+                x.y = fma(c, p[v].y, t.y);
+                *a = isr ? p[v] : x;
+            }
+    }
+
+    if (bid == 0 && threadIdx.x == 0) {
+        const int64_t k = st->slot[s].k;
+        basis[rglob] = k;
+        const int64_t n = st->pivots;
+        if (logk && n < st->logcap) {
+            logk[n] = k;
+            logr[n] = rglob;
+        }
+        st->pivots = n + 1;
+        st->last_k = k;
+        st->last_r = rglob;
+    }
+}
+
+struct UpdateCfg {
+    int vpt, ru;
+    bool nt;
+    int strip;
+};
+
+static const UpdateCfg kUpdateCfgs[] = {
+    {1, 8, false, 64},   // 0: default
+    {2, 4, false, 64},   // 1
+    {1, 8, true, 64},    // 2: non-temporal
+    {2, 4, true, 64},    // 3
+    {1, 4, false, 32},   // 4
+    {4, 2, false, 64},   // 5
+};
+constexpr int kNumUpdateCfgs = sizeof(kUpdateCfgs) / sizeof(kUpdateCfgs[0]);
+
+int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
+                  int64_t *basis, int64_t *logk, int64_t *logr, int variant) {
+    if (variant < 0 || variant >= kNumUpdateCfgs) variant = 0;
+    const UpdateCfg cfg = kUpdateCfgs[variant];
+    const int64_t nvec = (g.ncols + 1) / 2;
+    const int64_t ntiles = (nvec + kBlock * cfg.vpt - 1) / (kBlock * cfg.vpt);
+    const int64_t nrows = g.nloc + g.nobj;
+    const int64_t nstrips = (nrows + cfg.strip - 1) / cfg.strip;
+    const int64_t nblocks = ntiles * nstrips;
+    if (nblocks > 0x7fffffff) return -1;
+    hipStream_t stream = (hipStream_t)L.stream;
+    dim3 grid((unsigned)nblocks), blk(kBlock);
+#define LPG_UPD(V, R, N) \
+    hipLaunchKernelGGL((k_update<V, R, N>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, ntiles, (int64_t)cfg.strip, basis, logk, logr)
+    switch (variant) {
+        case 1: LPG_UPD(2, 4, false); break;
+        case 2: LPG_UPD(1, 8, true); break;
+        case 3: LPG_UPD(2, 4, true); break;
+        case 4: LPG_UPD(1, 4, false); break;
+        case 5: LPG_UPD(4, 2, false); break;
+        default: LPG_UPD(1, 8, false); break;
+    }
+#undef LPG_UPD
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace lpg

@@ -1,0 +1,96 @@
+"""Row-block partition protocol, world_size 2 and 3, torch.distributed `gloo` on CPU.
+
+The multi-GPU engine (linearprogramming_amd/csrc/lpg_ctx.hip, `enqueue`)
+exchanges exactly two things per pivot: the ratio-test candidates
+(allgather) and the normalised pivot row (allreduce-sum of the owner's row
+and zeros). This test runs that protocol over real gloo collectives with the
+CPU oracle's row-block primitives on each rank and requires the pivot log and
+the final tableau to be bitwise identical to the single-process oracle.
+"""
+from __future__ import annotations
+
+import os
+import pickle
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle.lpo import GEN_DEGENERATE, GEN_DENSE, RULE_BLAND, RULE_DANTZIG, Oracle
+
+
+def _protocol_worker(rank, world, port, m, n, seed, kind, rule, max_pivots, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full = Oracle(m, n + m + 1)
+        full.generate(n, seed, kind)
+        T = full.get_rows()
+        basis = full.get_basis()
+        row0, row1 = m * rank // world, m * (rank + 1) // world
+        blk = Oracle(row1 - row0, n + m + 1)
+        blk.load_tableau(np.vstack([T[row0:row1], T[m:m + 1]]), basis[row0:row1])
+        log, status = [], "ITER_LIMIT"
+        for _ in range(max_pivots):
+            k = blk.price_col(rule)
+            if k < 0:
+                status = "OPTIMAL"
+                break
+            cand = torch.from_numpy(blk.ratio(k, rule, row0))
+            gathered = [torch.zeros(4, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(gathered, cand)
+            valid = [g.numpy() for g in gathered if g[3] >= 0]
+            if not valid:
+                status = "UNBOUNDED"
+                break
+            best = min(valid, key=lambda c: (c[0], c[2]))
+            r = int(best[3])
+            rl = r - row0 if row0 <= r < row1 else -1
+            P = torch.from_numpy(blk.pivot_row(rl, k)) if rl >= 0 else torch.zeros(n + m + 1, dtype=torch.float64)
+            dist.all_reduce(P, op=dist.ReduceOp.SUM)
+            blk.apply(k, rl, P.numpy())
+            log.append((k, r))
+        rows = blk.get_rows()
+        with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+            pickle.dump({"log": log, "status": status, "rows": rows[:-1], "obj": rows[-1],
+                         "basis": blk.get_basis()}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world,m,n,kind,rule", [
+    (2, 40, 64, GEN_DENSE, RULE_DANTZIG),
+    (2, 33, 50, GEN_DEGENERATE, RULE_BLAND),
+    (3, 47, 61, GEN_DENSE, RULE_DANTZIG),
+])
+def test_gloo_row_partition_matches_single_process(world, m, n, kind, rule):
+    seed, max_pivots = 12345, 4000
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_protocol_worker, args=(world, _free_port(), m, n, seed, kind, rule, max_pivots, d),
+                 nprocs=world, join=True)
+        parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
+    ref = Oracle(m, n + m + 1)
+    ref.generate(n, seed, kind)
+    res = ref.solve(max_pivots, rule)
+    k, r = ref.get_log()
+    expect_log = list(zip(k.tolist(), r.tolist()))
+    T = ref.get_rows()
+    for p in parts:
+        assert p["log"] == expect_log
+        assert p["status"] == {1: "OPTIMAL", 2: "UNBOUNDED", 4: "ITER_LIMIT"}[res.status]
+        assert np.array_equal(p["obj"], T[m])            # replicated objective row identical on every rank
+    assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
+    assert np.concatenate([p["basis"] for p in parts]).tolist() == ref.get_basis().tolist()

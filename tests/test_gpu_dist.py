@@ -1,0 +1,155 @@
+"""Multi-rank HIP engine on the one-GPU box.
+
+The engine's row-block protocol (allgather of ratio candidates, allreduce of
+the owner's normalised pivot row) runs through lpg_comm_init_host:
+* in one process, 2-3 ranks as threads sharing the GPU with an in-process
+  host transport;
+* in 2 processes with torch.distributed `gloo` collectives on host tensors
+  (the RCCL transport itself needs one GPU per rank and runs in the driver's
+  8-GPU bench).
+Every rank's pivot log, basis and replicated objective row, and the stacked
+row blocks, must equal the single-rank engine and the oracle bitwise.
+"""
+from __future__ import annotations
+
+import os
+import pickle
+import socket
+import tempfile
+import threading
+
+import numpy as np
+import pytest
+
+from oracle.lpo import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+class ThreadComm:
+    """In-process allgather / allreduce-sum for ranks running as threads."""
+
+    def __init__(self, world):
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.slots = [None] * world
+
+    def allgather(self, rank, data: bytes) -> bytes:
+        self.slots[rank] = data
+        self.bar.wait()
+        out = b"".join(self.slots)
+        self.bar.wait()
+        return out
+
+    def allreduce(self, rank, arr: np.ndarray) -> np.ndarray:
+        self.slots[rank] = arr
+        self.bar.wait()
+        acc = self.slots[0].copy()
+        for q in range(1, self.world):
+            acc = acc + self.slots[q]
+        self.bar.wait()
+        return acc
+
+
+def _run_threads(lpg, world, m, n, seed, kind, rule, max_pivots):
+    comm = ThreadComm(world)
+    out = [None] * world
+    errs = []
+
+    def worker(rank):
+        try:
+            e = lpg.Engine(m, n + m + 1, world=world, rank=rank)
+            e.comm_init_host(lambda b: comm.allgather(rank, b), lambda a: comm.allreduce(rank, a))
+            e.generate(n, seed, kind)
+            res = e.solve(max_pivots, rule)
+            info = e.info
+            out[rank] = dict(res=res, log=e.get_log(), basis=e.get_basis(),
+                             rows=e.get_rows(info.row0, info.nrows), obj=e.get_rows(m, 1)[0])
+            e.close()
+        except Exception as ex:   # pragma: no cover
+            errs.append(ex)
+            comm.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(600)
+    assert not errs, errs
+    return out
+
+
+@pytest.fixture(scope="module")
+def lpg():
+    import linearprogramming_amd as lpg
+    lpg.load()
+    return lpg
+
+
+@pytest.mark.parametrize("world,m,n,kind,rule", [(2, 96, 160, 0, 0), (3, 101, 77, 0, 0), (2, 64, 64, 1, 1)])
+def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule):
+    seed = 777
+    parts = _run_threads(lpg, world, m, n, seed, kind, rule, 100_000)
+    o = Oracle(m, n + m + 1)
+    o.generate(n, seed, kind)
+    ores = o.solve(100_000, rule)
+    k, r = o.get_log()
+    T = o.get_rows()
+    for p in parts:
+        assert p["res"].status == ores.status and p["res"].pivots == ores.pivots
+        assert np.array_equal(p["log"][0], k) and np.array_equal(p["log"][1], r)
+        assert np.array_equal(p["basis"], o.get_basis())
+        assert np.array_equal(p["obj"], T[m])
+    assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
+
+
+def _gloo_worker(rank, world, port, m, n, seed, outdir):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import linearprogramming_amd as lpg
+
+    def allgather(b: bytes) -> bytes:
+        t = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return b"".join(bytes(o.numpy()) for o in outs)
+
+    def allreduce(a: np.ndarray) -> np.ndarray:
+        t = torch.from_numpy(a)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.numpy()
+
+    e = lpg.Engine(m, n + m + 1, world=world, rank=rank)
+    e.comm_init_host(allgather, allreduce)
+    e.generate(n, seed, 0)
+    res = e.solve(100_000, 0)
+    info = e.info
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(dict(status=res.status, pivots=res.pivots, log=e.get_log(),
+                         rows=e.get_rows(info.row0, info.nrows), obj=e.get_rows(m, 1)[0]), f)
+    e.close()
+    dist.destroy_process_group()
+
+
+def test_two_processes_gloo_bitwise(lpg):
+    import torch.multiprocessing as mp
+    m, n, seed = 120, 200, 31
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_gloo_worker, args=(2, port, m, n, seed, d), nprocs=2, join=True)
+        parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(2)]
+    o = Oracle(m, n + m + 1)
+    o.generate(n, seed, 0)
+    ores = o.solve(100_000, 0)
+    T = o.get_rows()
+    for p in parts:
+        assert p["status"] == ores.status and p["pivots"] == ores.pivots
+        assert np.array_equal(p["log"][0], o.get_log()[0])
+        assert np.array_equal(p["obj"], T[m])
+    assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
