@@ -31,7 +31,7 @@ def lpg():
 
 
 def _pair(lpg, m, ncols, **kw):
-    return lpg.Engine(m, ncols, **kw), Oracle(m, ncols, nthreads=os.cpu_count() or 1)
+    return lpg.Engine(m, ncols, **kw), Oracle(m, ncols, nthreads=int(os.environ.get("OMP_NUM_THREADS", "8")))
 
 
 def _log(x):
