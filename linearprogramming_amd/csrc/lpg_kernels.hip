@@ -396,7 +396,7 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
     if (!FIRST) {
         r = st->slot[s].r;
         kc = st->slot[s].k;
-        rl = r - g.row0;
+        rl = (r >= g.row0 && r < g.row0 + g.nloc) ? r - g.row0 : -1;
         p0 = P[0];
         pk = P[kn];
     }
@@ -469,7 +469,9 @@ __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g
     const int32_t status = st->slot[s].status;
     if (status != RUNNING) return;
     const int64_t rglob = st->slot[s].r;
-    const int64_t rl = rglob - g.row0;
+    // local index of the pivot row, -1 on a non-owner rank (never alias the
+    // objective row at local index nloc)
+    const int64_t rl = (rglob >= g.row0 && rglob < g.row0 + g.nloc) ? rglob - g.row0 : -1;
     const int64_t bid = blockIdx.x;
     const int64_t tile = bid % ntiles;
     const int64_t strip = bid / ntiles;

@@ -89,10 +89,10 @@ def lpg():
 @pytest.mark.parametrize("world,m,n,kind,rule", [(2, 96, 160, 0, 0), (3, 101, 77, 0, 0), (2, 64, 64, 1, 1)])
 def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule):
     seed = 777
-    parts = _run_threads(lpg, world, m, n, seed, kind, rule, 100_000)
+    parts = _run_threads(lpg, world, m, n, seed, kind, rule, 5000)
     o = Oracle(m, n + m + 1)
     o.generate(n, seed, kind)
-    ores = o.solve(100_000, rule)
+    ores = o.solve(5000, rule)
     k, r = o.get_log()
     T = o.get_rows()
     for p in parts:
@@ -125,7 +125,7 @@ def _gloo_worker(rank, world, port, m, n, seed, outdir):
     e = lpg.Engine(m, n + m + 1, world=world, rank=rank)
     e.comm_init_host(allgather, allreduce)
     e.generate(n, seed, 0)
-    res = e.solve(100_000, 0)
+    res = e.solve(5000, 0)
     info = e.info
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump(dict(status=res.status, pivots=res.pivots, log=e.get_log(),
@@ -146,7 +146,7 @@ def test_two_processes_gloo_bitwise(lpg):
         parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(2)]
     o = Oracle(m, n + m + 1)
     o.generate(n, seed, 0)
-    ores = o.solve(100_000, 0)
+    ores = o.solve(5000, 0)
     T = o.get_rows()
     for p in parts:
         assert p["status"] == ores.status and p["pivots"] == ores.pivots
