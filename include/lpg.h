@@ -65,7 +65,7 @@ extern "C" {
 
 /* ---- synthetic generators (device-side) ---- */
 #define LPG_GEN_DENSE      0  /* A_ij = u, b_i = n/8 (1+u), c_j = 1+u, <= rows, slack basis */
-#define LPG_GEN_DEGENERATE 1  /* lower-triangular KM-style rows, b_i = 0 on even rows     */
+#define LPG_GEN_DEGENERATE 1  /* lower-triangular KM-style rows (a_ii = 1, a_ij = u/(i+1)), b_i = 0 on even rows */
 
 /* ---- lpg_create flags ---- */
 #define LPG_FLAG_NO_LOG  0x1u  /* do not record the (entering, leaving) pivot log */

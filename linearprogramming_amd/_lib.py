@@ -92,6 +92,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         return _lib
     if not os.path.exists(path):
         raise RuntimeError(f"lpg HIP engine not built: {path} is missing (run `make` or __graft_entry__.build())")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same
+    # soname as /opt/rocm's). Loading torch first makes liblpg bind to the
+    # runtime torch will use; the reverse order (liblpg first, torch later)
+    # aborts at interpreter exit on the box (tools/runtime_order.py).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, res, args in PROTOTYPES:
         fn = getattr(lib, name)

@@ -157,7 +157,7 @@ __global__ __launch_bounds__(kBlock) void k_generate(double *__restrict__ T, Geo
                 if (kind == 0) {
                     x = uniform01(kA, (uint64_t)(gi * n + jj));
                 } else {
-                    if (jj < gi) x = 2.0 * uniform01(kA, (uint64_t)(gi * n + jj));
+                    if (jj < gi) x = uniform01(kA, (uint64_t)(gi * n + jj)) / (double)(gi + 1);
                     else if (jj == gi) x = 1.0;
                 }
             } else if (j == 1 + n + gi) {

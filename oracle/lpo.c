@@ -119,7 +119,10 @@ int lpo_set_active_columns(lpo_ctx *c, int64_t nact) {
 
 /* Synthetic LPs. Dense: A_ij = u in [0,1), b_i = n/8 (1+u),
  * c_j = 1+u, all rows <= with a slack basis. Degenerate: lower-triangular
- * KM-style rows (a_ii = 1, a_ij = 2u for j < i), b_i = 0 on even rows. */
+ * KM-style rows (a_ii = 1, a_ij = u/(i+1) for j < i, so the strictly-lower
+ * part has infinity-norm < 1 and every basis inverse stays bounded; the 2u of
+ * SURVEY.md's sketch grows like 3^i and makes fp64 Bland cycle by m = 256),
+ * b_i = 0 on even rows (primal degenerate). */
 int lpo_generate(lpo_ctx *c, int64_t n, uint64_t seed, int kind) {
     if (!c || n < 1 || c->ncols != n + c->m + 1) return -1;
     const int64_t m = c->m, ld = c->ld;
@@ -136,7 +139,7 @@ int lpo_generate(lpo_ctx *c, int64_t n, uint64_t seed, int kind) {
             row[0] = (i & 1) ? bscale * (1.0 + lpo_uniform(kB, (uint64_t)i)) : 0.0;
             for (int64_t j = 0; j < n; j++) {
                 double a = 0.0;
-                if (j < i) a = 2.0 * lpo_uniform(kA, (uint64_t)(i * n + j));
+                if (j < i) a = lpo_uniform(kA, (uint64_t)(i * n + j)) / (double)(i + 1);
                 else if (j == i) a = 1.0;
                 row[1 + j] = a;
             }

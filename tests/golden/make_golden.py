@@ -71,7 +71,7 @@ def synthetic(m: int, n: int, seed: int, kind: int):
         else:
             row[0] = bscale * (1.0 + uniform(kB, i)) if i & 1 else 0.0
             for j in range(n):
-                row[1 + j] = 2.0 * uniform(kA, i * n + j) if j < i else (1.0 if j == i else 0.0)
+                row[1 + j] = uniform(kA, i * n + j) / float(i + 1) if j < i else (1.0 if j == i else 0.0)
         row[1 + n + i] = 1.0
         T.append(row)
     obj = [0.0] * (n + m + 1)

@@ -104,7 +104,7 @@ def test_synthetic_exact_fixtures(lpg, case):
 
 
 @pytest.mark.parametrize("m,n,seed,kind,rule", [
-    (64, 96, 11, 0, 0), (200, 300, 12, 0, 0), (333, 517, 13, 0, 0), (256, 256, 14, 1, 1), (257, 100, 15, 1, 0),
+    (64, 96, 11, 0, 0), (200, 300, 12, 0, 0), (333, 517, 13, 0, 0), (48, 48, 14, 1, 1), (257, 100, 15, 1, 0),
     (1024, 2048, 20220518, 0, 0),   # BASELINE config 2, to optimality
 ])
 def test_to_optimality_bitwise(lpg, m, n, seed, kind, rule):
@@ -115,6 +115,20 @@ def test_to_optimality_bitwise(lpg, m, n, seed, kind, rule):
     ores = o.solve(200_000, rule)
     assert res.status == ores.status == STATUS["OPTIMAL"]
     assert res.pivots == ores.pivots > 0
+    assert res.objective == ores.objective
+    _assert_same(e, o, m)
+
+
+@pytest.mark.parametrize("m,cap", [(512, 3000), (2048, 400)])
+def test_bland_degenerate_capped(lpg, m, cap):
+    """KM-style degenerate LP (b_i = 0 on even rows) under Bland: the pivot count grows
+    exponentially with m (config 5 is pivot-capped); the capped runs agree bitwise."""
+    e, o = _pair(lpg, m, 2 * m + 1)
+    e.generate(m, 14, 1)
+    o.generate(m, 14, 1)
+    res = e.solve(cap, 1)
+    ores = o.solve(cap, 1)
+    assert res.status == ores.status and res.pivots == ores.pivots
     assert res.objective == ores.objective
     _assert_same(e, o, m)
 
