@@ -82,5 +82,6 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
                   int64_t *basis, int64_t *logk, int64_t *logr, int variant);
 
 int price_blocks(const Geo &g);      // number of pricing partials (= prep / price grid)
+int update_variants();               // entries of the update-kernel variant table
 
 }  // namespace lpg

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "lpg_internal.h"
 
 namespace lpg {
@@ -451,19 +453,63 @@ int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState 
 // ------------------------------------------------------------------------
 // update_t (a12): Gauss-Jordan rank-1 elimination, the HBM-bound hot loop.
 //
-// Block = 256 lanes x VPT 16-byte column slices (a 4*VPT KB column tile);
-// it walks a strip of SR rows. Each lane keeps its slice of the normalised
-// pivot row P in VGPRs for the whole strip (the register form of staging the
-// pivot row on chip: no lane ever needs another lane's P, so LDS would only
-// add a round trip). The per-row multiplier C[i] is wave-uniform and comes
-// through the scalar cache. RU rows are loaded before any is stored, so each
-// lane keeps RU*VPT 16-byte loads in flight.
+// Work item = (column tile, row strip). A tile is 256 lanes x VPT 16-byte
+// column slices (4*VPT KB of a row); a strip is SR rows. Each lane keeps its
+// slice of the normalised pivot row P in VGPRs for the whole strip (the
+// register form of staging the pivot row on chip: no lane ever needs another
+// lane's P, so LDS would only add a round trip). The per-row multiplier C[i]
+// is wave-uniform and comes through the scalar cache. RU rows are loaded
+// before any is stored (RU*VPT 16-byte loads in flight per lane); with PIPE
+// the next RU rows are loaded before the current ones are stored, so the
+// stream never drains between batches. With a persistent grid (PERSIST)
+// a fixed number of blocks per CU walks the items with a grid stride, which
+// removes the partial last wave of a one-block-per-item launch.
 // ------------------------------------------------------------------------
 
 template <int VPT, int RU, bool NT>
+__device__ __forceinline__ void upd_load(d2 (&t)[RU][VPT], const d2 *__restrict__ Tv, int64_t i, int64_t ld2,
+                                         int64_t cb, const bool (&ok)[VPT]) {
+#pragma unroll
+    for (int u = 0; u < RU; u++)
+#pragma unroll
+        for (int v = 0; v < VPT; v++)
+            if (ok[v]) {
+                const d2 *a = Tv + (i + u) * ld2 + cb + v * kBlock;
+                t[u][v] = NT ? __builtin_nontemporal_load(a) : *a;
+            }
+}
+
+template <int VPT, int RU, bool NT>
+__device__ __forceinline__ void upd_compute_store(d2 (&t)[RU][VPT], d2 *__restrict__ Tv, int64_t i, int64_t ld2,
+                                                  int64_t cb, const bool (&ok)[VPT], const d2 (&p)[VPT],
+                                                  const double *__restrict__ Cs, int64_t rl) {
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+        const double c = -Cs[i + u];
+        const bool isr = (i + u) == rl;
+#pragma unroll
+        for (int v = 0; v < VPT; v++) {
+            d2 x;
+            x.x = fma(c, p[v].x, t[u][v].x);
+            x.y = fma(c, p[v].y, t[u][v].y);
+            t[u][v] = isr ? p[v] : x;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < RU; u++)
+#pragma unroll
+        for (int v = 0; v < VPT; v++)
+            if (ok[v]) {
+                d2 *a = Tv + (i + u) * ld2 + cb + v * kBlock;
+                if (NT) __builtin_nontemporal_store(t[u][v], a);
+                else *a = t[u][v];
+            }
+}
+
+template <int VPT, int RU, bool NT, bool PIPE>
 __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g, DevState *__restrict__ st, int s,
                                                    const double *__restrict__ P, const double *__restrict__ Cs,
-                                                   int64_t ntiles, int64_t strip_rows,
+                                                   int64_t ntiles, int64_t strip_rows, int64_t nitems,
                                                    int64_t *__restrict__ basis, int64_t *__restrict__ logk,
                                                    int64_t *__restrict__ logr) {
     const int32_t status = st->slot[s].status;
@@ -472,75 +518,58 @@ __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g
     // local index of the pivot row, -1 on a non-owner rank (never alias the
     // objective row at local index nloc)
     const int64_t rl = (rglob >= g.row0 && rglob < g.row0 + g.nloc) ? rglob - g.row0 : -1;
-    const int64_t bid = blockIdx.x;
-    const int64_t tile = bid % ntiles;
-    const int64_t strip = bid / ntiles;
     const int64_t nrows = g.nloc + g.nobj;
-    const int64_t i0 = strip * strip_rows;
-    const int64_t i1 = i0 + strip_rows < nrows ? i0 + strip_rows : nrows;
     const int64_t nvec = (g.ncols + 1) / 2;
-    const int64_t cb = tile * (kBlock * VPT) + threadIdx.x;
     const int64_t ld2 = g.ld / 2;
     d2 *__restrict__ Tv = (d2 *)T;
     const d2 *__restrict__ Pv = (const d2 *)P;
 
-    d2 p[VPT];
-    bool ok[VPT];
+    for (int64_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+        const int64_t tile = item % ntiles;
+        const int64_t strip = item / ntiles;
+        const int64_t i0 = strip * strip_rows;
+        const int64_t i1 = i0 + strip_rows < nrows ? i0 + strip_rows : nrows;
+        const int64_t cb = tile * (kBlock * VPT) + threadIdx.x;
+        d2 p[VPT];
+        bool ok[VPT];
 #pragma unroll
-    for (int v = 0; v < VPT; v++) {
-        ok[v] = cb + v * kBlock < nvec;
-        p[v] = ok[v] ? Pv[cb + v * kBlock] : d2{0.0, 0.0};
-    }
-
-    int64_t i = i0;
-    for (; i + RU <= i1; i += RU) {
-        d2 t[RU][VPT];
+        for (int v = 0; v < VPT; v++) {
+            ok[v] = cb + v * kBlock < nvec;
+            p[v] = ok[v] ? Pv[cb + v * kBlock] : d2{0.0, 0.0};
+        }
+        int64_t i = i0;
+        if (PIPE) {
+            if (i + RU <= i1) {
+                d2 t[RU][VPT];
+                upd_load<VPT, RU, NT>(t, Tv, i, ld2, cb, ok);
+                for (;;) {
+                    const bool more = i + 2 * RU <= i1;
+                    d2 nx[RU][VPT];
+                    if (more) upd_load<VPT, RU, NT>(nx, Tv, i + RU, ld2, cb, ok);
+                    upd_compute_store<VPT, RU, NT>(t, Tv, i, ld2, cb, ok, p, Cs, rl);
+                    i += RU;
+                    if (!more) break;
 #pragma unroll
-        for (int u = 0; u < RU; u++)
+                    for (int u = 0; u < RU; u++)
 #pragma unroll
-            for (int v = 0; v < VPT; v++)
-                if (ok[v]) {
-                    d2 *a = Tv + (i + u) * ld2 + cb + v * kBlock;
-                    t[u][v] = NT ? __builtin_nontemporal_load(a) : *a;
+                        for (int v = 0; v < VPT; v++) t[u][v] = nx[u][v];
                 }
-#pragma unroll
-        for (int u = 0; u < RU; u++) {
-            const double c = -Cs[i + u];
-            const bool isr = (i + u) == rl;
-#pragma unroll
-            for (int v = 0; v < VPT; v++) {
-                d2 x;
-                x.x = fma(c, p[v].x, t[u][v].x);
-                x.y = fma(c, p[v].y, t[u][v].y);
-                t[u][v] = isr ? p[v] : x;
+            }
+        } else {
+            for (; i + RU <= i1; i += RU) {
+                d2 t[RU][VPT];
+                upd_load<VPT, RU, NT>(t, Tv, i, ld2, cb, ok);
+                upd_compute_store<VPT, RU, NT>(t, Tv, i, ld2, cb, ok, p, Cs, rl);
             }
         }
-#pragma unroll
-        for (int u = 0; u < RU; u++)
-#pragma unroll
-            for (int v = 0; v < VPT; v++)
-                if (ok[v]) {
-                    d2 *a = Tv + (i + u) * ld2 + cb + v * kBlock;
-                    if (NT) __builtin_nontemporal_store(t[u][v], a);
-                    else *a = t[u][v];
-                }
-    }
-    for (; i < i1; i++) {
-        const double c = -Cs[i];
-        const bool isr = i == rl;
-#pragma unroll
-        for (int v = 0; v < VPT; v++)
-            if (ok[v]) {
-                d2 *a = Tv + i * ld2 + cb + v * kBlock;
-                const d2 t = *a;
-                d2 x;
-                x.x = fma(c, p[v].x, t.x);
-                x.y = fma(c, p[v].y, t.y);
-                *a = isr ? p[v] : x;
-            }
+        for (; i < i1; i++) {
+            d2 t[1][VPT];
+            upd_load<VPT, 1, NT>(t, Tv, i, ld2, cb, ok);
+            upd_compute_store<VPT, 1, NT>(t, Tv, i, ld2, cb, ok, p, Cs, rl);
+        }
     }
 
-    if (bid == 0 && threadIdx.x == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         const int64_t k = st->slot[s].k;
         basis[rglob] = k;
         const int64_t n = st->pivots;
@@ -556,19 +585,31 @@ __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g
 
 struct UpdateCfg {
     int vpt, ru;
-    bool nt;
+    bool nt, pipe;
     int strip;
+    int persist;      // blocks per CU of a persistent grid; 0 = one block per item
 };
 
+// Variant table (LPG_UPDATE_VARIANT); every variant is bit-identical.
 static const UpdateCfg kUpdateCfgs[] = {
-    {1, 8, false, 64},   // 0: default
-    {2, 4, false, 64},   // 1
-    {1, 8, true, 64},    // 2: non-temporal
-    {2, 4, true, 64},    // 3
-    {1, 4, false, 32},   // 4
-    {4, 2, false, 64},   // 5
+    {1, 8, false, false, 64, 0},    // 0
+    {2, 4, false, false, 64, 0},    // 1
+    {1, 8, true, false, 64, 0},     // 2  non-temporal
+    {2, 4, true, false, 64, 0},     // 3
+    {1, 4, false, false, 32, 0},    // 4
+    {4, 2, false, false, 64, 0},    // 5
+    {1, 8, false, false, 64, 8},    // 6  persistent, 8 blocks/CU
+    {1, 4, false, true, 64, 0},     // 7  pipelined
+    {1, 8, false, true, 64, 0},     // 8
+    {1, 4, false, true, 64, 8},     // 9  pipelined + persistent
+    {2, 4, false, true, 64, 0},     // 10
+    {1, 8, true, true, 64, 0},      // 11 pipelined + non-temporal
+    {1, 16, false, false, 128, 0},  // 12
+    {1, 4, false, true, 256, 4},    // 13 tall strips, persistent 4/CU
 };
 constexpr int kNumUpdateCfgs = sizeof(kUpdateCfgs) / sizeof(kUpdateCfgs[0]);
+
+int update_variants() { return kNumUpdateCfgs; }
 
 int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
                   int64_t *basis, int64_t *logk, int64_t *logr, int variant) {
@@ -578,19 +619,30 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
     const int64_t ntiles = (nvec + kBlock * cfg.vpt - 1) / (kBlock * cfg.vpt);
     const int64_t nrows = g.nloc + g.nobj;
     const int64_t nstrips = (nrows + cfg.strip - 1) / cfg.strip;
-    const int64_t nblocks = ntiles * nstrips;
+    const int64_t nitems = ntiles * nstrips;
+    int64_t nblocks = nitems;
+    if (cfg.persist > 0) nblocks = std::min<int64_t>(nitems, (int64_t)256 * cfg.persist);
     if (nblocks > 0x7fffffff) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
     dim3 grid((unsigned)nblocks), blk(kBlock);
-#define LPG_UPD(V, R, N) \
-    hipLaunchKernelGGL((k_update<V, R, N>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, ntiles, (int64_t)cfg.strip, basis, logk, logr)
+#define LPG_UPD(V, R, N, PI)                                                                                  \
+    hipLaunchKernelGGL((k_update<V, R, N, PI>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, ntiles,           \
+                       (int64_t)cfg.strip, nitems, basis, logk, logr)
     switch (variant) {
-        case 1: LPG_UPD(2, 4, false); break;
-        case 2: LPG_UPD(1, 8, true); break;
-        case 3: LPG_UPD(2, 4, true); break;
-        case 4: LPG_UPD(1, 4, false); break;
-        case 5: LPG_UPD(4, 2, false); break;
-        default: LPG_UPD(1, 8, false); break;
+        case 1: LPG_UPD(2, 4, false, false); break;
+        case 2: LPG_UPD(1, 8, true, false); break;
+        case 3: LPG_UPD(2, 4, true, false); break;
+        case 4: LPG_UPD(1, 4, false, false); break;
+        case 5: LPG_UPD(4, 2, false, false); break;
+        case 6: LPG_UPD(1, 8, false, false); break;
+        case 7: LPG_UPD(1, 4, false, true); break;
+        case 8: LPG_UPD(1, 8, false, true); break;
+        case 9: LPG_UPD(1, 4, false, true); break;
+        case 10: LPG_UPD(2, 4, false, true); break;
+        case 11: LPG_UPD(1, 8, true, true); break;
+        case 12: LPG_UPD(1, 16, false, false); break;
+        case 13: LPG_UPD(1, 4, false, true); break;
+        default: LPG_UPD(1, 8, false, false); break;
     }
 #undef LPG_UPD
     return hipGetLastError() == hipSuccess ? 0 : -1;
