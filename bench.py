@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--variant", type=int, default=None, help="update-kernel variant (LPG_UPDATE_VARIANT)")
+    ap.add_argument("--force-rccl", action="store_true", help="attach a 1-rank RCCL communicator at N=1 (times the exchange)")
     return ap.parse_args()
 
 
@@ -104,6 +105,8 @@ def main():
         uid = [lpg.Engine.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init_rccl(uid[0])
+    elif a.force_rccl:
+        eng.comm_init_rccl(lpg.Engine.rccl_unique_id())
     eng.generate(n, SEED, lpg.GEN_DENSE)
     eng.reserve_log(a.warmup + a.steps + 8)
     eng.enqueue(a.warmup, lpg.RULE_DANTZIG)
@@ -146,7 +149,8 @@ def main():
         "data": f"synthetic dense LP generated on device (splitmix64 seed {SEED}): A_ij=u, b_i=n/8(1+u), c_j=1+u",
         "config": {"workload": cfg["name"], "m": m, "n": n, "tableau": [m + 1, n + m + 1],
                    "tableau_GB": (m + 1) * (n + m + 1) * 8 / 1e9, "rule": "dantzig",
-                   "parallelism": f"row-block x{world}" + (" (RCCL allgather + allreduce per pivot)" if world > 1 else ""),
+                   "parallelism": f"row-block x{world}" + (" (RCCL allgather + allreduce per pivot)"
+                                                           if world > 1 or a.force_rccl else ""),
                    "update_variant": int(os.environ.get("LPG_UPDATE_VARIANT", "0"))},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -115,6 +115,9 @@ int  lpg_create(lpg_ctx **out, int device, int64_t m, int64_t ncols, uint32_t fl
 int  lpg_create_dist(lpg_ctx **out, int device, int world, int rank,
                      int64_t m, int64_t ncols, uint32_t flags);
 int  lpg_comm_unique_id(void *uid, size_t len);              /* RCCL id, len >= 128 */
+/* Attach an RCCL communicator (all ranks call it together). A world-1
+ * context may attach one too: the per-pivot collectives then run for real on
+ * a 1-rank communicator (used to test and time the exchange on one GPU). */
 int  lpg_comm_init_rccl(lpg_ctx *ctx, const void *uid, size_t len);
 int  lpg_comm_init_host(lpg_ctx *ctx, const lpg_host_comm_ops *ops);
 /* Replaces RevokeSMatrix (matrix.c:97-123). NULL is a no-op. */

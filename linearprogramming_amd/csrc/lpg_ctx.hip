@@ -117,8 +117,10 @@ static int use_device(lpg_ctx *c) {
 // collectives: RCCL on device buffers, or caller-provided host-staged ops
 // ---------------------------------------------------------------------------
 
+static bool has_comm(const lpg_ctx *c) { return c->world > 1 || c->nccl || c->have_hops; }
+
 static int comm_allgather(lpg_ctx *c, const void *send, void *recv, size_t bytes) {
-    if (c->world == 1) return 0;
+    if (!has_comm(c)) return 0;
     if (c->nccl) {
         ncclResult_t r = ncclAllGather(send, recv, bytes, ncclUint8, c->nccl, c->stream);
         if (r != ncclSuccess) return fail(c, LPG_ERR_COMM, "ncclAllGather: %s", ncclGetErrorString(r));
@@ -137,7 +139,7 @@ static int comm_allgather(lpg_ctx *c, const void *send, void *recv, size_t bytes
 }
 
 static int comm_allreduce_sum(lpg_ctx *c, double *buf, size_t count) {
-    if (c->world == 1) return 0;
+    if (!has_comm(c)) return 0;
     if (c->nccl) {
         ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, c->nccl, c->stream);
         if (r != ncclSuccess) return fail(c, LPG_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
@@ -190,7 +192,7 @@ static int timing_mark(lpg_ctx *c, int which) {
 // ---------------------------------------------------------------------------
 
 static int exchange_candidates(lpg_ctx *c) {
-    if (c->world == 1) return 0;
+    if (!has_comm(c)) return 0;
     return comm_allgather(c, c->part, c->cand, sizeof(Cand) * (size_t)c->nsel);
 }
 
@@ -217,7 +219,9 @@ static int enqueue(lpg_ctx *c, int64_t npiv, int rule) {
     }
     const Geo g = geo(c);
     const Launch L = lau(c);
-    const bool fuse = c->world == 1;
+    // Without a communicator the pricing of d_{t+1} is fused into prep; with
+    // one (any world size) P must be exchanged first.
+    const bool fuse = !has_comm(c);
     const int ncand = c->nsel * c->world;
     for (int64_t q = 0; q < npiv; q++) {
         const int s = c->par, s1 = s ^ 1;
@@ -407,7 +411,7 @@ int lpg_comm_unique_id(void *uid, size_t len) {
 
 int lpg_comm_init_rccl(lpg_ctx *c, const void *uid, size_t len) {
     if (!c || !uid || len < sizeof(ncclUniqueId)) return fail(c, LPG_ERR_ARG, "bad uid");
-    if (c->world == 1) return 0;
+    if (c->nccl || c->have_hops) return fail(c, LPG_ERR_STATE, "communicator already attached");
     int rc;
     if ((rc = use_device(c))) return rc;
     ncclUniqueId id;
@@ -422,6 +426,7 @@ int lpg_comm_init_rccl(lpg_ctx *c, const void *uid, size_t len) {
 
 int lpg_comm_init_host(lpg_ctx *c, const lpg_host_comm_ops *ops) {
     if (!c || !ops || !ops->allgather || !ops->allreduce_sum_f64) return fail(c, LPG_ERR_ARG, "bad host comm ops");
+    if (c->nccl || c->have_hops) return fail(c, LPG_ERR_STATE, "communicator already attached");
     c->hops = *ops;
     c->have_hops = true;
     return 0;

@@ -153,3 +153,33 @@ def test_two_processes_gloo_bitwise(lpg):
         assert np.array_equal(p["log"][0], o.get_log()[0])
         assert np.array_equal(p["obj"], T[m])
     assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
+
+
+@pytest.mark.parametrize("m,n", [(300, 500), (1024, 2048)])
+def test_rccl_single_rank_communicator(lpg, m, n):
+    """The RCCL transport on a 1-rank communicator: every per-pivot ncclAllReduce
+    (pivot row) and ncclAllGather (ratio candidates) really runs, and the result
+    is bitwise the engine without a communicator (and the oracle)."""
+    e = lpg.Engine(m, n + m + 1)
+    e.comm_init_rccl(lpg.Engine.rccl_unique_id())
+    e.generate(n, 41, 0)
+    res = e.solve(100_000, 0)
+    o = Oracle(m, n + m + 1)
+    o.generate(n, 41, 0)
+    ores = o.solve(100_000, 0)
+    assert res.status == ores.status == 1 and res.pivots == ores.pivots and res.objective == ores.objective
+    assert np.array_equal(e.get_log()[0], o.get_log()[0]) and np.array_equal(e.get_log()[1], o.get_log()[1])
+    assert np.array_equal(e.get_rows(0, m + 1), o.get_rows())
+
+
+def test_host_comm_single_rank(lpg):
+    e = lpg.Engine(50, 50 + 70 + 1)
+    e.comm_init_host(lambda b: b, lambda a: a)
+    e.generate(70, 42, 0)
+    res = e.solve(10_000, 0)
+    o = Oracle(50, 50 + 70 + 1)
+    o.generate(70, 42, 0)
+    ores = o.solve(10_000, 0)
+    assert res.pivots == ores.pivots and np.array_equal(e.get_rows(0, 51), o.get_rows())
+    with pytest.raises(lpg.LPGError):
+        e.comm_init_host(lambda b: b, lambda a: a)     # one communicator per context
