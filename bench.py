@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--variant", type=int, default=None, help="update-kernel variant (LPG_UPDATE_VARIANT)")
+    ap.add_argument("--no-skip", action="store_true", help="update every column (disable column skipping)")
     ap.add_argument("--force-rccl", action="store_true", help="attach a 1-rank RCCL communicator at N=1 (times the exchange)")
     return ap.parse_args()
 
@@ -85,6 +86,8 @@ def main():
     a = parse()
     if a.variant is not None:
         os.environ["LPG_UPDATE_VARIANT"] = str(a.variant)
+    if a.no_skip:
+        os.environ["LPG_NO_SKIP"] = "1"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -133,7 +136,10 @@ def main():
         elapsed = float(tt.item())
 
     upd_ms = timing.update_ms / max(timing.update_count, 1)
-    achieved = info.bytes_per_pivot / (upd_ms * 1e-3) / 1e9 if upd_ms > 0 else 0.0
+    # bytes the update kernel actually read + wrote (skipped all-zero P slices
+    # are not counted); == bytes_per_pivot without skipping
+    touched = timing.update_bytes / max(timing.update_count, 1)
+    achieved = touched / (upd_ms * 1e-3) / 1e9 if upd_ms > 0 else 0.0
     line = {
         "metric": METRIC,
         "value": a.steps / elapsed,
@@ -155,7 +161,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "lpg::k_update (Gauss-Jordan rank-1)",
-                     "algorithmic_bytes_per_launch": info.bytes_per_pivot,
+                     "algorithmic_bytes_per_launch": touched,
+                     "full_tableau_bytes_per_launch": info.bytes_per_pivot,
+                     "column_skipping": not a.no_skip,
                      "update_ms_mean": upd_ms,
                      "other_ms_mean": timing.select_ms / max(timing.update_count, 1)},
         "status": lpg.STATUS_NAMES.get(res.status, res.status),

@@ -69,6 +69,7 @@ extern "C" {
 
 /* ---- lpg_create flags ---- */
 #define LPG_FLAG_NO_LOG  0x1u  /* do not record the (entering, leaving) pivot log */
+#define LPG_FLAG_NO_SKIP 0x2u  /* update every column (no skipping of P[j] == 0 slices) */
 
 typedef struct lpg_ctx lpg_ctx;
 
@@ -96,6 +97,9 @@ typedef struct {
     double  select_ms;          /* summed device time of pricing + ratio-test kernels */
     double  comm_ms;            /* summed device time of the collectives */
     int64_t update_count;       /* update launches timed */
+    double  update_bytes;       /* bytes the update kernels read + wrote (16-byte slices whose
+                                   pivot-row entries are not both zero, x rows, x 2); equals
+                                   update_count * bytes_per_pivot when nothing is skipped */
 } lpg_timing;
 
 /* Host-staged collectives supplied by the caller (tests, non-RCCL transports).

@@ -20,6 +20,7 @@ STATUS_NAMES = {0: "RUNNING", 1: "OPTIMAL", 2: "UNBOUNDED", 3: "INFEASIBLE", 4: 
 RULE_DANTZIG, RULE_BLAND = 0, 1
 GEN_DENSE, GEN_DEGENERATE = 0, 1
 FLAG_NO_LOG = 0x1
+FLAG_NO_SKIP = 0x2
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int64_p = ctypes.POINTER(ctypes.c_int64)
@@ -40,7 +41,7 @@ class Info(ctypes.Structure):
 
 class Timing(ctypes.Structure):
     _fields_ = [("update_ms", ctypes.c_double), ("select_ms", ctypes.c_double),
-                ("comm_ms", ctypes.c_double), ("update_count", ctypes.c_int64)]
+                ("comm_ms", ctypes.c_double), ("update_count", ctypes.c_int64), ("update_bytes", ctypes.c_double)]
 
 
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)

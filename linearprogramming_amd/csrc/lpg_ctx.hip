@@ -63,6 +63,8 @@ struct lpg_ctx {
     int par = 0;                  // parity of the next pivot's slot
     int64_t enq = 0;              // pivots enqueued since the last reset (log bound)
     int update_variant = 0;
+    int skip = 1;                 // column skipping in the update (LPG_FLAG_NO_SKIP turns it off)
+    unsigned long long touched_mark = 0;
     // communication
     ncclComm_t nccl = nullptr;
     lpg_host_comm_ops hops{};
@@ -239,7 +241,7 @@ static int enqueue(lpg_ctx *c, int64_t npiv, int rule) {
             return fail(c, LPG_ERR_DEVICE, "select launch failed");
         if ((rc = exchange_candidates(c))) return rc;
         if (c->timing && (rc = timing_mark(c, 1))) return rc;
-        if (launch_update(L, g, c->st, s, c->P, c->C[s], c->basis, c->logk, c->logr, c->update_variant))
+        if (launch_update(L, g, c->st, s, c->P, c->C[s], c->basis, c->logk, c->logr, c->update_variant, c->skip))
             return fail(c, LPG_ERR_DEVICE, "update launch failed");
         if (c->timing && (rc = timing_mark(c, 2))) return rc;
         c->par = s1;
@@ -276,6 +278,7 @@ static int reset_state(lpg_ctx *c) {
     c->booted = false;
     c->par = 0;
     c->enq = 0;
+    c->touched_mark = 0;
     return 0;
 }
 
@@ -343,6 +346,8 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->flags = flags;
     const char *uv = getenv("LPG_UPDATE_VARIANT");
     c->update_variant = uv ? atoi(uv) : 0;
+    const char *ns = getenv("LPG_NO_SKIP");
+    c->skip = ((flags & LPG_FLAG_NO_SKIP) || (ns && atoi(ns))) ? 0 : 1;
     int rc;
     if ((rc = use_device(c))) { lpg_destroy(c); return rc; }
     const int64_t rows = c->nloc + c->nobj;
@@ -673,6 +678,10 @@ int lpg_get_timing(lpg_ctx *c, lpg_timing *out) {
     int rc;
     if ((rc = use_device(c))) return rc;
     if ((rc = timing_flush(c))) return rc;
+    unsigned long long touched = 0;
+    HIPCHK(c, hipMemcpy(&touched, &c->st->touched, sizeof touched, hipMemcpyDeviceToHost));
+    out->update_bytes = 32.0 * (double)(touched - c->touched_mark);
+    c->touched_mark = touched;
     out->update_ms = c->tr.update_ms;
     out->select_ms = c->tr.select_ms;
     out->comm_ms = c->tr.comm_ms;

@@ -34,6 +34,7 @@ struct DevState {
     int64_t pivots;           // pivots applied (update kernels that ran)
     int64_t last_k, last_r;
     int64_t logcap;
+    unsigned long long touched;   // 16-byte slices the update read+wrote (column skipping accounting)
 };
 
 // Ratio-test candidate: lexicographic (theta, key); row < 0 = none.
@@ -79,7 +80,7 @@ int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState 
                   const double *P, const double *Cs, double *Cs1, const PricePart *pp, int npp,
                   const int64_t *basis, Cand *part, int nsel);
 int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
-                  int64_t *basis, int64_t *logk, int64_t *logr, int variant);
+                  int64_t *basis, int64_t *logk, int64_t *logr, int variant, int skip);
 
 int price_blocks(const Geo &g);      // number of pricing partials (= prep / price grid)
 int update_variants();               // entries of the update-kernel variant table

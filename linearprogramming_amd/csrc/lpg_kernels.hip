@@ -511,7 +511,7 @@ __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g
                                                    const double *__restrict__ P, const double *__restrict__ Cs,
                                                    int64_t ntiles, int64_t strip_rows, int64_t nitems,
                                                    int64_t *__restrict__ basis, int64_t *__restrict__ logk,
-                                                   int64_t *__restrict__ logr) {
+                                                   int64_t *__restrict__ logr, int skip) {
     const int32_t status = st->slot[s].status;
     if (status != RUNNING) return;
     const int64_t rglob = st->slot[s].r;
@@ -532,11 +532,20 @@ __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g
         const int64_t cb = tile * (kBlock * VPT) + threadIdx.x;
         d2 p[VPT];
         bool ok[VPT];
+        int live = 0;
 #pragma unroll
         for (int v = 0; v < VPT; v++) {
             ok[v] = cb + v * kBlock < nvec;
             p[v] = ok[v] ? Pv[cb + v * kBlock] : d2{0.0, 0.0};
+            // Column skipping: where both P
+            // entries are zero the update leaves the slice's values unchanged
+            // (fma(-c, 0, t) == t; only the sign of a zero could differ), so
+            // the slice is neither read nor written. Basic columns other than
+            // the leaving one always have P == 0.
+            if (skip && p[v].x == 0.0 && p[v].y == 0.0) ok[v] = false;
+            live += ok[v] ? 1 : 0;
         }
+        const int64_t i0c = i0, i1c = i1;
         int64_t i = i0;
         if (PIPE) {
             if (i + RU <= i1) {
@@ -567,6 +576,12 @@ __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g
             upd_load<VPT, 1, NT>(t, Tv, i, ld2, cb, ok);
             upd_compute_store<VPT, 1, NT>(t, Tv, i, ld2, cb, ok, p, Cs, rl);
         }
+        // touched-bytes accounting: one 64-bit atomic per work item
+        int wl = live;
+#pragma unroll
+        for (int mask = 32; mask > 0; mask >>= 1) wl += __shfl_xor(wl, mask, 64);
+        if ((threadIdx.x & 63) == 0 && wl)
+            atomicAdd(&st->touched, (unsigned long long)wl * (unsigned long long)(i1c - i0c));
     }
 
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -612,7 +627,7 @@ constexpr int kNumUpdateCfgs = sizeof(kUpdateCfgs) / sizeof(kUpdateCfgs[0]);
 int update_variants() { return kNumUpdateCfgs; }
 
 int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
-                  int64_t *basis, int64_t *logk, int64_t *logr, int variant) {
+                  int64_t *basis, int64_t *logk, int64_t *logr, int variant, int skip) {
     if (variant < 0 || variant >= kNumUpdateCfgs) variant = 0;
     const UpdateCfg cfg = kUpdateCfgs[variant];
     const int64_t nvec = (g.ncols + 1) / 2;
@@ -627,7 +642,7 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
     dim3 grid((unsigned)nblocks), blk(kBlock);
 #define LPG_UPD(V, R, N, PI)                                                                                  \
     hipLaunchKernelGGL((k_update<V, R, N, PI>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, ntiles,           \
-                       (int64_t)cfg.strip, nitems, basis, logk, logr)
+                       (int64_t)cfg.strip, nitems, basis, logk, logr, skip)
     switch (variant) {
         case 1: LPG_UPD(2, 4, false, false); break;
         case 2: LPG_UPD(1, 8, true, false); break;

@@ -224,6 +224,27 @@ def test_update_variants_identical(lpg, variant, monkeypatch):
     _assert_same(e, o, m)
 
 
+@pytest.mark.parametrize("m,n,kind,rule,piv", [(500, 900, 0, 0, 300), (300, 300, 1, 1, 2000)])
+def test_column_skipping_is_value_identical(lpg, m, n, kind, rule, piv, monkeypatch):
+    """Skipping slices whose pivot-row entries are zero changes no value (np.array_equal;
+    only the sign of a zero may differ) and no decision; the touched-bytes counter is
+    exact without skipping and smaller with it."""
+    e = lpg.Engine(m, n + m + 1)
+    monkeypatch.setenv("LPG_NO_SKIP", "1")
+    f = lpg.Engine(m, n + m + 1)
+    monkeypatch.delenv("LPG_NO_SKIP")
+    for x in (e, f):
+        x.generate(n, 51, kind)
+        x.set_timing(True)
+        x.get_timing()
+        x.solve(piv, rule)
+    te, tf = e.get_timing(), f.get_timing()
+    assert _log(e) == _log(f)
+    assert np.array_equal(e.get_rows(0, m + 1), f.get_rows(0, m + 1))
+    assert tf.update_bytes == tf.update_count * f.info.bytes_per_pivot
+    assert 0 < te.update_bytes < tf.update_bytes
+
+
 def test_timing_counters(lpg):
     e = lpg.Engine(512, 512 + 1024 + 1)
     e.generate(1024, 25, 0)
