@@ -66,6 +66,8 @@ extern "C" {
 /* ---- synthetic generators (device-side) ---- */
 #define LPG_GEN_DENSE      0  /* A_ij = u, b_i = n/8 (1+u), c_j = 1+u, <= rows, slack basis */
 #define LPG_GEN_DEGENERATE 1  /* lower-triangular KM-style rows (a_ii = 1, a_ij = u/(i+1)), b_i = 0 on even rows */
+#define LPG_GEN_ARTIFICIAL 2  /* config 5: KM-style; even rows `<= 0` (a_ij = -u/(i+1)), odd rows equalities whose
+                                 unit columns are artificials at columns 1+n+ceil(m/2) .. N */
 
 /* ---- lpg_create flags ---- */
 #define LPG_FLAG_NO_LOG  0x1u  /* do not record the (entering, leaving) pivot log */
@@ -140,7 +142,8 @@ int  lpg_set_basis(lpg_ctx *ctx, const int64_t *basis);
 /* Objective row from costs c[0..N-1] of `max c.x` and the current basis:
  * d_j = sum_i c_B(i) T[i][j] - c_j, z = sum_i c_B(i) b_i, summed in global
  * row order with fma (bitwise independent of the partition). Replaces
- * SimplexMatrix.ofCosts / basicCosts (matrix.c:55-57, 76-77). */
+ * SimplexMatrix.ofCosts / basicCosts (matrix.c:55-57, 76-77). The pivot
+ * count and log are kept (phase I -> phase II). */
 int  lpg_set_objective(lpg_ctx *ctx, const double *c);
 int  lpg_set_tolerances(lpg_ctx *ctx, double eps_piv, double eps_opt);
 /* Price only columns 1..nact (e.g. to exclude artificials). */
@@ -161,6 +164,22 @@ int  lpg_sync(lpg_ctx *ctx, lpg_result *out);
 /* Pre-size the device pivot log for npivots more pivots so that no
  * reallocation (and host synchronisation) happens inside a timed region. */
 int  lpg_reserve_log(lpg_ctx *ctx, int64_t npivots);
+
+/* Apply one caller-chosen pivot (entering column k, 1-based; leaving row r,
+ * 0-based) with the same arithmetic as the loop; |T[r][k]| must exceed
+ * eps_piv (either sign). Counts as a pivot and is logged. */
+int  lpg_pivot(lpg_ctx *ctx, int64_t k, int64_t r);
+/* Two-phase method for a tableau whose columns art_first..N are artificial
+ * unit columns basic in the rows that lacked an identity column
+ * (reference: the empty `case 2:` of simplex.c:61-62, lack list from
+ * matrix.c:80-89). Phase I maximises -sum(artificials); a negative optimum
+ * means LPG_INFEASIBLE. Artificials left basic at zero are pivoted out on the
+ * first usable original column of their row. Phase II prices columns
+ * 1..art_first-1 only, with the objective row recomputed from cost[0..N-1]
+ * (cost NULL: -1 x the objective row as loaded, i.e. a slack-form -c row).
+ * Single rank. */
+int  lpg_solve_two_phase(lpg_ctx *ctx, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
+                         lpg_result *out);
 
 /* ---- readout ---- */
 int  lpg_get_rows(lpg_ctx *ctx, int64_t row0, int64_t nrows, double *out, int64_t ld);

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -205,6 +206,21 @@ static int bootstrap(lpg_ctx *c, int rule) {
         return fail(c, LPG_ERR_DEVICE, "price launch failed");
     if (launch_select(lau(c), g, rule, true, c->st, 0, 0, c->P, c->C[1], c->C[0], c->pp, c->npp, c->basis,
                       c->part, c->nsel))
+        return fail(c, LPG_ERR_DEVICE, "select launch failed");
+    int rc = exchange_candidates(c);
+    if (rc) return rc;
+    c->par = 0;
+    c->booted = true;
+    c->boot_rule = rule;
+    return 0;
+}
+
+// Bootstrap onto a caller-chosen pivot (k, r): no pricing, the ratio test
+// admits only row r (either sign, |T[r][k]| > eps_piv).
+static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
+    HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
+    if (launch_select(lau(c), geo(c), rule, true, c->st, 0, 0, c->P, c->C[1], c->C[0], c->pp, c->npp, c->basis,
+                      c->part, c->nsel, k, r))
         return fail(c, LPG_ERR_DEVICE, "select launch failed");
     int rc = exchange_candidates(c);
     if (rc) return rc;
@@ -525,7 +541,8 @@ int lpg_set_objective(lpg_ctx *c, const double *cost) {
     }
     if (launch_objective_finish(lau(c), g, chain, c->cost)) return fail(c, LPG_ERR_DEVICE, "objective finish failed");
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return reset_state(c);
+    c->booted = false;   // re-price from the new objective row; the pivot count and log carry on
+    return 0;
 }
 
 int lpg_set_tolerances(lpg_ctx *c, double eps_piv, double eps_opt) {
@@ -544,7 +561,7 @@ int lpg_set_active_columns(lpg_ctx *c, int64_t nact) {
 }
 
 int lpg_generate(lpg_ctx *c, int64_t n, uint64_t seed, int kind) {
-    if (!c || n < 1 || c->ncols != n + c->m + 1 || (kind != LPG_GEN_DENSE && kind != LPG_GEN_DEGENERATE))
+    if (!c || n < 1 || c->ncols != n + c->m + 1 || kind < LPG_GEN_DENSE || kind > LPG_GEN_ARTIFICIAL)
         return fail(c, LPG_ERR_ARG, "lpg_generate: need ncols == n + m + 1 and a known kind");
     int rc;
     if ((rc = use_device(c))) return rc;
@@ -603,6 +620,84 @@ int lpg_solve(lpg_ctx *c, int64_t max_pivots, int rule, lpg_result *out) {
         batch = std::min<int64_t>(batch * 2, 256);
     }
     return read_result(c, out, rule);
+}
+
+int lpg_pivot(lpg_ctx *c, int64_t k, int64_t r) {
+    if (!c || k < 1 || k >= c->ncols || r < 0 || r >= c->m) return fail(c, LPG_ERR_ARG, "lpg_pivot: bad (k, r)");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    if ((rc = ensure_log(c, c->enq + 1))) return rc;
+    const int rule = c->booted ? c->boot_rule : LPG_RULE_DANTZIG;
+    lpg_result before, after;
+    if ((rc = read_result(c, &before, rule))) return rc;
+    if ((rc = bootstrap_forced(c, rule, k, r))) return rc;
+    if ((rc = enqueue(c, 1, rule))) return rc;
+    if ((rc = read_result(c, &after, rule))) return rc;
+    c->booted = false;   // the next solve prices from scratch
+    if (after.pivots != before.pivots + 1)
+        return fail(c, LPG_ERR_STATE, "lpg_pivot: |T[%lld][%lld]| <= eps_piv, pivot not applied", (long long)r, (long long)k);
+    return 0;
+}
+
+int lpg_solve_two_phase(lpg_ctx *c, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
+                        lpg_result *out) {
+    if (!c || art_first < 2 || art_first >= c->ncols || max_pivots < 0)
+        return fail(c, LPG_ERR_ARG, "lpg_solve_two_phase: bad arguments");
+    if (c->world != 1) return fail(c, LPG_ERR_STATE, "lpg_solve_two_phase: single rank only");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    const int64_t N = c->ncols - 1;
+    std::vector<double> own;
+    if (!cost) {   // costs = -1 x the objective row as loaded (slack-form -c row)
+        own.resize(c->ncols);
+        if ((rc = lpg_get_rows(c, c->m, 1, own.data(), c->ncols))) return rc;
+        for (int64_t j = 1; j <= N; j++) own[j - 1] = -own[j];
+        cost = own.data();
+    }
+    // Phase I: max -sum(artificials) over all columns.
+    std::vector<double> c1(N, 0.0);
+    for (int64_t j = art_first; j <= N; j++) c1[j - 1] = -1.0;
+    if ((rc = lpg_set_active_columns(c, N)) || (rc = lpg_set_objective(c, c1.data()))) return rc;
+    lpg_result r1;
+    if ((rc = lpg_solve(c, max_pivots, rule, &r1))) return rc;
+    int64_t used = r1.pivots;
+    if (r1.status == LPG_ITER_LIMIT || r1.status == LPG_NUMERIC || r1.status == LPG_UNBOUNDED) {
+        if (out) { *out = r1; if (r1.status == LPG_UNBOUNDED) out->status = LPG_NUMERIC; }
+        return 0;
+    }
+    // infeasible when the artificials cannot all reach zero
+    double bsum = 0;
+    {
+        std::vector<double> xb(c->nloc);
+        if ((rc = lpg_get_column0(c, xb.data()))) return rc;
+        for (double v : xb) bsum += fabs(v);
+    }
+    if (r1.objective < -1e-9 * std::max(1.0, bsum)) {
+        if (out) { *out = r1; out->status = LPG_INFEASIBLE; }
+        return 0;
+    }
+    // Drive artificials still basic (at zero) out of the basis with forced
+    // degenerate pivots on the first usable original column of their row; a
+    // row with no such column is redundant and keeps its artificial at zero.
+    std::vector<int64_t> basis(c->m);
+    if ((rc = lpg_get_basis(c, basis.data()))) return rc;
+    std::vector<double> row(c->ncols);
+    for (int64_t i = 0; i < c->m; i++) {
+        if (basis[i] < art_first) continue;
+        if ((rc = lpg_get_rows(c, i, 1, row.data(), c->ncols))) return rc;
+        for (int64_t j = 1; j < art_first; j++)
+            if (fabs(row[j]) > c->eps_piv) {
+                if ((rc = lpg_pivot(c, j, i))) return rc;
+                used++;
+                break;
+            }
+    }
+    // Phase II: original costs, artificial columns barred from entering.
+    if ((rc = lpg_set_active_columns(c, art_first - 1)) || (rc = lpg_set_objective(c, cost))) return rc;
+    lpg_result r2;
+    if ((rc = lpg_solve(c, std::max<int64_t>(max_pivots - used, 0), rule, &r2))) return rc;
+    if (out) *out = r2;
+    return 0;
 }
 
 int lpg_get_rows(lpg_ctx *c, int64_t row0, int64_t nrows, double *out, int64_t ld) {

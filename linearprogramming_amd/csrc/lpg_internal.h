@@ -78,7 +78,7 @@ int launch_prep(const Launch &L, const Geo &g, int rule, bool fuse_price, DevSta
                 const Cand *cand, int ncand, double *P, const double *Cs, PricePart *pp, int npp);
 int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState *st, int s, int s1,
                   const double *P, const double *Cs, double *Cs1, const PricePart *pp, int npp,
-                  const int64_t *basis, Cand *part, int nsel);
+                  const int64_t *basis, Cand *part, int nsel, int64_t force_k = 0, int64_t force_r = -1);
 int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
                   int64_t *basis, int64_t *logk, int64_t *logr, int variant, int skip);
 

@@ -135,6 +135,14 @@ static inline uint64_t subkey(uint64_t seed, uint64_t which) {
     return splitmix64_host(seed ^ (which * 0xD1B54A32D192ED03ull));
 }
 
+// Column of row i's initial unit column (oracle lpo_unit_column): kinds 0/1
+// slack 1+n+i; kind 2 slacks of even rows first, then the artificials of the
+// odd (equality) rows from art_first = 1+n+ceil(m/2).
+__host__ __device__ __forceinline__ int64_t unit_column(int64_t m, int64_t n, int64_t i, int kind) {
+    if (kind != 2) return 1 + n + i;
+    return (i & 1) ? 1 + n + (m + 1) / 2 + i / 2 : 1 + n + i / 2;
+}
+
 // grid: x = local row, y = chunk of 512 columns (256 lanes x 2). Every rank
 // fills all m basis entries (slack basis) through k_basis_slack.
 __global__ __launch_bounds__(kBlock) void k_generate(double *__restrict__ T, Geo g, int64_t n, uint64_t kA,
@@ -159,10 +167,11 @@ __global__ __launch_bounds__(kBlock) void k_generate(double *__restrict__ T, Geo
                 if (kind == 0) {
                     x = uniform01(kA, (uint64_t)(gi * n + jj));
                 } else {
-                    if (jj < gi) x = uniform01(kA, (uint64_t)(gi * n + jj)) / (double)(gi + 1);
+                    const double sgn = (kind == 2 && !(gi & 1)) ? -1.0 : 1.0;
+                    if (jj < gi) x = sgn * (uniform01(kA, (uint64_t)(gi * n + jj)) / (double)(gi + 1));
                     else if (jj == gi) x = 1.0;
                 }
-            } else if (j == 1 + n + gi) {
+            } else if (j == unit_column(g.m, n, gi, kind)) {
                 x = 1.0;
             }
         } else if (i == g.nloc) {
@@ -173,9 +182,9 @@ __global__ __launch_bounds__(kBlock) void k_generate(double *__restrict__ T, Geo
     *(d2 *)(row + j0) = d2{v[0], v[1]};
 }
 
-__global__ void k_basis_slack(int64_t *__restrict__ basis, int64_t m, int64_t n) {
+__global__ void k_basis_slack(int64_t *__restrict__ basis, int64_t m, int64_t n, int kind) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < m) basis[i] = 1 + n + i;
+    if (i < m) basis[i] = unit_column(m, n, i, kind);
 }
 
 int launch_generate(const Launch &L, const Geo &g, int64_t n, uint64_t seed, int kind, int64_t *basis_dev) {
@@ -187,7 +196,7 @@ int launch_generate(const Launch &L, const Geo &g, int64_t n, uint64_t seed, int
     hipLaunchKernelGGL(k_generate, grid, dim3(kBlock), 0, st, g.T, g, n, subkey(seed, 1), subkey(seed, 2),
                        subkey(seed, 3), kind);
     hipLaunchKernelGGL(k_basis_slack, dim3((unsigned)((g.m + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
-                       basis_dev, g.m, n);
+                       basis_dev, g.m, n, kind);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -360,7 +369,8 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
                                                    int s1, const double *__restrict__ P,
                                                    const double *__restrict__ Cs, double *__restrict__ Cs1,
                                                    const PricePart *__restrict__ pp, int npp,
-                                                   const int64_t *__restrict__ basis, Cand *__restrict__ part) {
+                                                   const int64_t *__restrict__ basis, Cand *__restrict__ part,
+                                                   int64_t force_k, int64_t force_r) {
     Slot *dst = &st->slot[s1];
     if (!FIRST) {
         const int32_t stt = st->slot[s].status;
@@ -374,12 +384,17 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
         }
     }
     PricePart pb{0.0, -1};
-    for (int q = threadIdx.x; q < npp; q += kBlock) {
-        const PricePart c = pp[q];
-        if (pp_better<RULE>(c, pb)) pb = c;
+    if (force_k > 0) {              // forced pivot (lpg_pivot): no pricing
+        pb.j = force_k;
+        pb.v = -1.0;
+    } else {
+        for (int q = threadIdx.x; q < npp; q += kBlock) {
+            const PricePart c = pp[q];
+            if (pp_better<RULE>(c, pb)) pb = c;
+        }
+        pb = block_reduce_pp<RULE>(pb);
     }
-    pb = block_reduce_pp<RULE>(pb);
-    const bool optimal = pb.j < 0 || (RULE == RULE_DANTZIG && !(pb.v < -g.eps_opt));
+    const bool optimal = pb.j < 0 || (force_k <= 0 && RULE == RULE_DANTZIG && !(pb.v < -g.eps_opt));
     if (optimal) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             dst->status = OPTIMAL;
@@ -420,7 +435,8 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
             a = fma(c, pk, oa);
         }
         Cs1[i] = a;
-        if (i < g.nloc && a > g.eps_piv) {
+        const bool eligible = force_r >= 0 ? (g.row0 + i == force_r && fabs(a) > g.eps_piv) : a > g.eps_piv;
+        if (i < g.nloc && eligible) {
             const int64_t grow = g.row0 + i;
             Cand c;
             c.theta = b > 0.0 ? b / a : 0.0;
@@ -436,11 +452,12 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
 
 int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState *st, int s, int s1, const double *P,
                   const double *Cs, double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part,
-                  int nsel) {
+                  int nsel, int64_t force_k, int64_t force_r) {
     hipStream_t stream = (hipStream_t)L.stream;
     dim3 grid(nsel), blk(kBlock);
-#define LPG_SEL(R, F) \
-    hipLaunchKernelGGL((k_select<R, F>), grid, blk, 0, stream, g.T, g, st, s, s1, P, Cs, Cs1, pp, npp, basis, part)
+#define LPG_SEL(R, F)                                                                                     \
+    hipLaunchKernelGGL((k_select<R, F>), grid, blk, 0, stream, g.T, g, st, s, s1, P, Cs, Cs1, pp, npp, basis, \
+                       part, force_k, force_r)
     if (rule == RULE_BLAND) {
         if (first) LPG_SEL(RULE_BLAND, true); else LPG_SEL(RULE_BLAND, false);
     } else {

@@ -167,6 +167,16 @@ class Engine:
         self._check(self.lib.lpg_sync(self._ctx, ctypes.byref(r)), "lpg_sync")
         return _res(r)
 
+    def pivot(self, k: int, r: int):
+        self._check(self.lib.lpg_pivot(self._ctx, k, r), "lpg_pivot")
+
+    def solve_two_phase(self, art_first: int, cost=None, max_pivots: int = 1 << 40, rule: int = L.RULE_DANTZIG):
+        cp = None if cost is None else np.ascontiguousarray(cost, dtype=np.float64).ctypes.data_as(L.c_double_p)
+        r = L.Result()
+        self._check(self.lib.lpg_solve_two_phase(self._ctx, art_first, cp, max_pivots, rule, ctypes.byref(r)),
+                    "lpg_solve_two_phase")
+        return _res(r)
+
     def reserve_log(self, n: int):
         self._check(self.lib.lpg_reserve_log(self._ctx, n), "lpg_reserve_log")
 

@@ -13,6 +13,7 @@
 #include "lpo.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -117,14 +118,25 @@ int lpo_set_active_columns(lpo_ctx *c, int64_t nact) {
     return 0;
 }
 
+/* Column of row i's initial unit (basic) column. Kinds 0/1: slack 1+n+i.
+ * Kind 2: even rows (<= 0, degenerate) get slacks 1+n+i/2, odd rows
+ * (equalities) get artificials from art_first = 1+n+ceil(m/2) on. */
+int64_t lpo_unit_column(int64_t m, int64_t n, int64_t i, int kind) {
+    if (kind != LPO_GEN_ARTIFICIAL) return 1 + n + i;
+    return (i & 1) ? 1 + n + (m + 1) / 2 + i / 2 : 1 + n + i / 2;
+}
+
 /* Synthetic LPs. Dense: A_ij = u in [0,1), b_i = n/8 (1+u),
  * c_j = 1+u, all rows <= with a slack basis. Degenerate: lower-triangular
  * KM-style rows (a_ii = 1, a_ij = u/(i+1) for j < i, so the strictly-lower
  * part has infinity-norm < 1 and every basis inverse stays bounded; the 2u of
  * SURVEY.md's sketch grows like 3^i and makes fp64 Bland cycle by m = 256),
- * b_i = 0 on even rows (primal degenerate). */
+ * b_i = 0 on even rows (primal degenerate). Artificial (config 5): as
+ * degenerate, but even rows have negative off-diagonals (a feasible
+ * `<= 0` row) and odd rows are equalities whose unit columns are artificial
+ * (columns art_first..N); the objective row still holds -c. */
 int lpo_generate(lpo_ctx *c, int64_t n, uint64_t seed, int kind) {
-    if (!c || n < 1 || c->ncols != n + c->m + 1) return -1;
+    if (!c || n < 1 || c->ncols != n + c->m + 1 || kind < 0 || kind > LPO_GEN_ARTIFICIAL) return -1;
     const int64_t m = c->m, ld = c->ld;
     const uint64_t kA = lpo_subkey(seed, 1), kB = lpo_subkey(seed, 2), kC = lpo_subkey(seed, 3);
     const double bscale = (double)n / 8.0;
@@ -137,15 +149,17 @@ int lpo_generate(lpo_ctx *c, int64_t n, uint64_t seed, int kind) {
             for (int64_t j = 0; j < n; j++) row[1 + j] = lpo_uniform(kA, (uint64_t)(i * n + j));
         } else {
             row[0] = (i & 1) ? bscale * (1.0 + lpo_uniform(kB, (uint64_t)i)) : 0.0;
+            const double sgn = (kind == LPO_GEN_ARTIFICIAL && !(i & 1)) ? -1.0 : 1.0;
             for (int64_t j = 0; j < n; j++) {
                 double a = 0.0;
-                if (j < i) a = lpo_uniform(kA, (uint64_t)(i * n + j)) / (double)(i + 1);
+                if (j < i) a = sgn * (lpo_uniform(kA, (uint64_t)(i * n + j)) / (double)(i + 1));
                 else if (j == i) a = 1.0;
                 row[1 + j] = a;
             }
         }
-        row[1 + n + i] = 1.0;
-        c->basis[i] = 1 + n + i;
+        const int64_t u = lpo_unit_column(m, n, i, kind);
+        row[u] = 1.0;
+        c->basis[i] = u;
     }
     double *obj = c->T + m * ld;
     memset(obj, 0, (size_t)ld * sizeof(double));
@@ -322,5 +336,50 @@ int lpo_apply(lpo_ctx *c, int64_t k, int64_t rl, const double *P) {
     }
     if (rl >= 0) c->basis[rl] = k;
     c->pivots++;
+    return 0;
+}
+
+/* Two-phase restatement (same algorithm as lpg_solve_two_phase). */
+int lpo_solve_two_phase(lpo_ctx *c, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
+                        lpo_result *out) {
+    if (!c || art_first < 2 || art_first >= c->ncols) return -1;
+    const int64_t N = c->ncols - 1;
+    double *own = NULL;
+    if (!cost) {
+        own = (double *)malloc((size_t)N * sizeof(double));
+        if (!own) return -1;
+        for (int64_t j = 1; j <= N; j++) own[j - 1] = -c->T[c->m * c->ld + j];
+        cost = own;
+    }
+    double *c1 = (double *)calloc((size_t)N, sizeof(double));
+    if (!c1) return -1;
+    for (int64_t j = art_first; j <= N; j++) c1[j - 1] = -1.0;
+    c->nact = N;
+    lpo_set_objective(c, c1);
+    free(c1);
+    lpo_result r1;
+    lpo_solve(c, max_pivots, rule, 1, &r1);
+    if (r1.status == LPO_ITER_LIMIT || r1.status == LPO_NUMERIC || r1.status == LPO_UNBOUNDED) {
+        if (out) { *out = r1; if (r1.status == LPO_UNBOUNDED) out->status = LPO_NUMERIC; }
+        free(own);
+        return 0;
+    }
+    double bsum = 0;
+    for (int64_t i = 0; i < c->m; i++) bsum += fabs(c->T[i * c->ld]);
+    if (r1.objective < -1e-9 * (bsum > 1.0 ? bsum : 1.0)) {
+        if (out) { *out = r1; out->status = LPO_INFEASIBLE; }
+        free(own);
+        return 0;
+    }
+    for (int64_t i = 0; i < c->m; i++) {
+        if (c->basis[i] < art_first) continue;
+        for (int64_t j = 1; j < art_first; j++)
+            if (fabs(c->T[i * c->ld + j]) > c->eps_piv) { lpo_pivot(c, j, i); break; }
+    }
+    c->nact = art_first - 1;
+    lpo_set_objective(c, cost);
+    int64_t left = max_pivots - c->pivots;
+    lpo_solve(c, left > 0 ? left : 0, rule, 1, out);
+    free(own);
     return 0;
 }

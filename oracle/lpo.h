@@ -44,7 +44,7 @@ extern "C" {
 enum { LPO_RUNNING = 0, LPO_OPTIMAL = 1, LPO_UNBOUNDED = 2, LPO_INFEASIBLE = 3,
        LPO_ITER_LIMIT = 4, LPO_NUMERIC = 5 };
 enum { LPO_RULE_DANTZIG = 0, LPO_RULE_BLAND = 1 };
-enum { LPO_GEN_DENSE = 0, LPO_GEN_DEGENERATE = 1 };
+enum { LPO_GEN_DENSE = 0, LPO_GEN_DEGENERATE = 1, LPO_GEN_ARTIFICIAL = 2 };
 
 typedef struct lpo_ctx lpo_ctx;
 
@@ -66,6 +66,7 @@ int      lpo_set_basis(lpo_ctx *ctx, const int64_t *basis);
  * d_j = sum_i c_B(i) T[i][j] - c_j, z = sum_i c_B(i) b_i (row order fixed). */
 int      lpo_set_objective(lpo_ctx *ctx, const double *c);
 int      lpo_generate(lpo_ctx *ctx, int64_t n_struct, uint64_t seed, int kind);
+int64_t  lpo_unit_column(int64_t m, int64_t n, int64_t i, int kind);
 int      lpo_set_tolerances(lpo_ctx *ctx, double eps_piv, double eps_opt);
 int      lpo_set_active_columns(lpo_ctx *ctx, int64_t nact);
 /* Run up to max_pivots pivots. nparts > 1 emulates the row-block partition of
@@ -82,6 +83,11 @@ int64_t  lpo_ld(const lpo_ctx *ctx);
 /* Rank-1 update only (timing harness for the CPU baseline): applies pivot
  * (k, r) with the bitwise contract above, no pricing or ratio test. */
 int      lpo_pivot(lpo_ctx *ctx, int64_t k, int64_t r);
+
+/* Two-phase method, same algorithm as lpg_solve_two_phase (cost NULL: the
+ * costs are -1 x the objective row as loaded, i.e. a slack-form -c row). */
+int      lpo_solve_two_phase(lpo_ctx *ctx, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
+                             lpo_result *out);
 
 /* Row-block primitives for the multi-rank protocol model (tests only). */
 int64_t  lpo_price_col(const lpo_ctx *ctx, int rule);

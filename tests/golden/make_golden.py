@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import json
 import os
+import re
 import subprocess
 import sys
 from fractions import Fraction
@@ -70,16 +71,24 @@ def synthetic(m: int, n: int, seed: int, kind: int):
                 row[1 + j] = uniform(kA, i * n + j)
         else:
             row[0] = bscale * (1.0 + uniform(kB, i)) if i & 1 else 0.0
+            sgn = -1.0 if (kind == 2 and not i & 1) else 1.0
             for j in range(n):
-                row[1 + j] = uniform(kA, i * n + j) / float(i + 1) if j < i else (1.0 if j == i else 0.0)
-        row[1 + n + i] = 1.0
+                row[1 + j] = sgn * (uniform(kA, i * n + j) / float(i + 1)) if j < i else (1.0 if j == i else 0.0)
+        row[unit_column(m, n, i, kind)] = 1.0
         T.append(row)
     obj = [0.0] * (n + m + 1)
     for j in range(n):
         obj[1 + j] = -(1.0 + uniform(kC, j))
     T.append(obj)
-    basis = [1 + n + i for i in range(m)]
+    basis = [unit_column(m, n, i, kind) for i in range(m)]
     return T, basis
+
+
+def unit_column(m: int, n: int, i: int, kind: int) -> int:
+    """Initial unit column of row i (kind 2: even-row slacks, then odd-row artificials)."""
+    if kind != 2:
+        return 1 + n + i
+    return 1 + n + (m + 1) // 2 + i // 2 if i & 1 else 1 + n + i // 2
 
 
 def frac_str(x: Fraction) -> str:
@@ -101,7 +110,9 @@ def transcripts():
             stdin = "\n"
         p = subprocess.run([REF_BIN, os.path.join("tests", "golden", "lp", name)], input=stdin,
                            capture_output=True, text=True, timeout=20, cwd=ROOT, env={"TERM": "dumb", "PATH": "/usr/bin:/bin"})
-        out[name] = {"stdin": stdin, "stdout": p.stdout, "returncode": p.returncode}
+        # the parse timer (main.c:20-23) is the only non-deterministic line
+        stdout = re.sub(r"Parsed in [0-9.]+s\.", "Parsed in 0.000000s.", p.stdout)
+        out[name] = {"stdin": stdin, "stdout": stdout, "returncode": p.returncode}
     return out
 
 
