@@ -42,6 +42,8 @@ CONFIGS = {
     2: dict(m=1024, n=2048, name="BASELINE config 2: random dense LP m=1024 n=2048 fp64"),
     3: dict(m=16384, n=32768, name="BASELINE config 3: random dense LP m=16384 n=32768 fp64"),
     4: dict(m=65536, n=131072, name="BASELINE config 4: random dense LP m=65536 n=131072 fp64"),
+    5: dict(m=8192, n=8192, name="BASELINE config 5: two-phase (artificials) on a KM-style degenerate LP m=8192 n=8192, "
+                                 "Bland rule, pivot cap 20000"),
 }
 
 
@@ -82,8 +84,66 @@ def cpu_baseline(m, n, gpu_log, budget_s):
             "seconds": dt}, {"pivots_compared": int(n_cmp), "identical_pivot_sequence": same}
 
 
+def config5(a):
+    """Config 5: the whole two-phase solve (phase I, artificial clean-up, phase II) under Bland."""
+    cfg = CONFIGS[5]
+    m, n, cap = cfg["m"], cfg["n"], 20000
+    art_first = 1 + n + (m + 1) // 2
+    eng = lpg.Engine(m, n + m + 1)
+    eng.generate(n, SEED, lpg.GEN_ARTIFICIAL)
+    eng.reserve_log(cap + 8)
+    eng.set_timing(True)
+    eng.get_timing()
+    eng.device_sync()
+    t0 = time.perf_counter()
+    res = eng.solve_two_phase(art_first, None, cap, lpg.RULE_BLAND)
+    eng.device_sync()
+    elapsed = time.perf_counter() - t0
+    timing = eng.get_timing()
+    upd_ms = timing.update_ms / max(timing.update_count, 1)
+    touched = timing.update_bytes / max(timing.update_count, 1)
+    achieved = touched / (upd_ms * 1e-3) / 1e9 if upd_ms > 0 else 0.0
+    line = {"metric": METRIC + " [config 5 variant: pivots/s of a full two-phase solve]", "value": res.pivots / elapsed,
+            "unit": "pivots/s", "n_gpus": 1, "steps": res.pivots, "warmup": 0,
+            "ms_per_step": elapsed / max(res.pivots, 1) * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64",
+            "data": f"synthetic KM-style degenerate LP with equality rows (splitmix64 seed {SEED}), generated on device",
+            "config": {"workload": cfg["name"], "m": m, "n": n, "rule": "bland", "art_first": art_first},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "lpg::k_update",
+                         "algorithmic_bytes_per_launch": touched,
+                         "full_tableau_bytes_per_launch": eng.info.bytes_per_pivot, "update_ms_mean": upd_ms},
+            "status": lpg.STATUS_NAMES.get(res.status, res.status), "pivots_total": res.pivots,
+            "objective": res.objective, "seconds": elapsed}
+    if not a.no_cpu:
+        from oracle.lpo import Oracle
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        o = Oracle(m, n + m + 1, nthreads=threads)
+        o.generate(n, SEED, 2)
+        k_cpu = 400
+        t0 = time.perf_counter()
+        ro = o.solve_two_phase(art_first, None, k_cpu, lpg.RULE_BLAND)
+        dt = time.perf_counter() - t0
+        ok, orr = o.get_log()
+        ek, er = eng.get_log()
+        ncmp = min(len(ok), len(ek))
+        line["cpu_baseline"] = {"value": ro.pivots / dt, "unit": "pivots/s", "cores": threads, "kind": "port",
+                                "sample": f"first {ro.pivots} pivots of the same two-phase solve (oracle/liblpo.so, "
+                                          f"OpenMP {threads} threads)", "seconds": dt}
+        line["parity"] = {"pivots_compared": int(ncmp),
+                          "identical_pivot_sequence": bool((ok[:ncmp] == ek[:ncmp]).all() and
+                                                           (orr[:ncmp] == er[:ncmp]).all())}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     a = parse()
+    if a.config == 5:
+        if a.gpus != 1:
+            raise SystemExit("config 5 (two-phase) is single-GPU")
+        if a.no_skip:
+            os.environ["LPG_NO_SKIP"] = "1"
+        return config5(a)
     if a.variant is not None:
         os.environ["LPG_UPDATE_VARIANT"] = str(a.variant)
     if a.no_skip:
