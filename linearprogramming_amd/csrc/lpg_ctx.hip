@@ -71,6 +71,11 @@ struct lpg_ctx {
     lpg_host_comm_ops hops{};
     bool have_hops = false;
     std::vector<unsigned char> hsend, hrecv;
+    // hipGraph of kGraphPivots pivots (starting at parity 0), replayed by
+    // enqueue when no communicator and no per-pivot timing is active
+    hipGraphExec_t graph = nullptr;
+    int graph_rule = -1;
+    bool use_graphs = true;
     // timing
     bool timing = false;
     TimingRing tr;
@@ -230,11 +235,62 @@ static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
     return 0;
 }
 
+static constexpr int kGraphPivots = 32;
+
+static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule);
+
+static void graph_drop(lpg_ctx *c) {
+    if (c->graph) (void)hipGraphExecDestroy(c->graph);
+    c->graph = nullptr;
+    c->graph_rule = -1;
+}
+
+// Capture kGraphPivots pivots starting at parity 0 (the launches read every
+// per-pivot choice from device memory, so one graph serves every replay).
+static int graph_build(lpg_ctx *c, int rule) {
+    graph_drop(c);
+    hipGraph_t g = nullptr;
+    HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    const int par = c->par;
+    const int64_t enq = c->enq;
+    c->par = 0;
+    int rc = enqueue_eager(c, kGraphPivots, rule);
+    hipError_t e = hipStreamEndCapture(c->stream, &g);
+    c->par = par;
+    c->enq = enq;
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(c, LPG_ERR_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(e));
+    e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) {
+        c->graph = nullptr;
+        return fail(c, LPG_ERR_DEVICE, "hipGraphInstantiate: %s", hipGetErrorString(e));
+    }
+    c->graph_rule = rule;
+    return 0;
+}
+
 static int enqueue(lpg_ctx *c, int64_t npiv, int rule) {
     if (!c->booted || c->boot_rule != rule) {
         int rc = bootstrap(c, rule);
         if (rc) return rc;
     }
+    if (!c->use_graphs || c->timing || has_comm(c) || npiv < 2 * kGraphPivots) return enqueue_eager(c, npiv, rule);
+    int rc;
+    if (c->par == 1) {                       // graphs start at parity 0
+        if ((rc = enqueue_eager(c, 1, rule))) return rc;
+        npiv--;
+    }
+    if (!c->graph || c->graph_rule != rule)
+        if ((rc = graph_build(c, rule))) return rc;
+    for (; npiv >= kGraphPivots; npiv -= kGraphPivots) {
+        HIPCHK(c, hipGraphLaunch(c->graph, c->stream));
+        c->enq += kGraphPivots;
+    }
+    return enqueue_eager(c, npiv, rule);
+}
+
+static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
     const Geo g = geo(c);
     const Launch L = lau(c);
     // Without a communicator the pricing of d_{t+1} is fused into prep; with
@@ -362,6 +418,8 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->flags = flags;
     const char *uv = getenv("LPG_UPDATE_VARIANT");
     c->update_variant = uv ? atoi(uv) : 0;
+    const char *ng = getenv("LPG_NO_GRAPH");
+    c->use_graphs = !(ng && atoi(ng));
     const char *ns = getenv("LPG_NO_SKIP");
     c->skip = ((flags & LPG_FLAG_NO_SKIP) || (ns && atoi(ns))) ? 0 : 1;
     int rc;
@@ -457,6 +515,7 @@ void lpg_destroy(lpg_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    graph_drop(c);
     if (c->nccl) ncclCommDestroy(c->nccl);
     for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
@@ -550,6 +609,7 @@ int lpg_set_tolerances(lpg_ctx *c, double eps_piv, double eps_opt) {
     c->eps_piv = eps_piv;
     c->eps_opt = eps_opt;
     c->booted = false;
+    graph_drop(c);
     return 0;
 }
 
@@ -557,6 +617,7 @@ int lpg_set_active_columns(lpg_ctx *c, int64_t nact) {
     if (!c || nact < 1 || nact > c->ncols - 1) return fail(c, LPG_ERR_ARG, "bad active column count");
     c->nact = nact;
     c->booted = false;
+    graph_drop(c);
     return 0;
 }
 

@@ -563,6 +563,8 @@ __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g
             live += ok[v] ? 1 : 0;
         }
         const int64_t i0c = i0, i1c = i1;
+        // a tile whose pivot-row slice is all zero is skipped as a whole
+        if (skip && !__syncthreads_or(live)) continue;
         int64_t i = i0;
         if (PIPE) {
             if (i + RU <= i1) {
@@ -638,6 +640,12 @@ static const UpdateCfg kUpdateCfgs[] = {
     {1, 8, true, true, 64, 0},      // 11 pipelined + non-temporal
     {1, 16, false, false, 128, 0},  // 12
     {1, 4, false, true, 256, 4},    // 13 tall strips, persistent 4/CU
+    {1, 8, true, false, 64, 8},     // 14 persistent + non-temporal
+    {2, 4, true, false, 64, 8},     // 15 2 slices/lane, persistent + non-temporal
+    {1, 8, false, false, 64, 4},    // 16 persistent 4/CU
+    {1, 8, true, true, 64, 8},      // 17 persistent + non-temporal + pipelined
+    {1, 8, false, false, 32, 8},    // 18 persistent, 32-row strips
+    {1, 8, true, false, 32, 8},     // 19 persistent + non-temporal, 32-row strips
 };
 constexpr int kNumUpdateCfgs = sizeof(kUpdateCfgs) / sizeof(kUpdateCfgs[0]);
 
@@ -650,7 +658,11 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
     const int64_t nvec = (g.ncols + 1) / 2;
     const int64_t ntiles = (nvec + kBlock * cfg.vpt - 1) / (kBlock * cfg.vpt);
     const int64_t nrows = g.nloc + g.nobj;
-    const int64_t nstrips = (nrows + cfg.strip - 1) / cfg.strip;
+    // Small tableaus: shrink the strip (down to RU rows) until there are at
+    // least ~4 work items per CU, so a config-2-sized update fills 256 CUs.
+    int64_t strip = cfg.strip;
+    while (strip > cfg.ru && strip > 8 && ntiles * ((nrows + strip - 1) / strip) < 1024) strip /= 2;
+    const int64_t nstrips = (nrows + strip - 1) / strip;
     const int64_t nitems = ntiles * nstrips;
     int64_t nblocks = nitems;
     if (cfg.persist > 0) nblocks = std::min<int64_t>(nitems, (int64_t)256 * cfg.persist);
@@ -658,8 +670,8 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
     hipStream_t stream = (hipStream_t)L.stream;
     dim3 grid((unsigned)nblocks), blk(kBlock);
 #define LPG_UPD(V, R, N, PI)                                                                                  \
-    hipLaunchKernelGGL((k_update<V, R, N, PI>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, ntiles,           \
-                       (int64_t)cfg.strip, nitems, basis, logk, logr, skip)
+    hipLaunchKernelGGL((k_update<V, R, N, PI>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, ntiles, strip,    \
+                       nitems, basis, logk, logr, skip)
     switch (variant) {
         case 1: LPG_UPD(2, 4, false, false); break;
         case 2: LPG_UPD(1, 8, true, false); break;
@@ -674,6 +686,12 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
         case 11: LPG_UPD(1, 8, true, true); break;
         case 12: LPG_UPD(1, 16, false, false); break;
         case 13: LPG_UPD(1, 4, false, true); break;
+        case 14: LPG_UPD(1, 8, true, false); break;
+        case 15: LPG_UPD(2, 4, true, false); break;
+        case 16: LPG_UPD(1, 8, false, false); break;
+        case 17: LPG_UPD(1, 8, true, true); break;
+        case 18: LPG_UPD(1, 8, false, false); break;
+        case 19: LPG_UPD(1, 8, true, false); break;
         default: LPG_UPD(1, 8, false, false); break;
     }
 #undef LPG_UPD

@@ -211,7 +211,7 @@ def test_set_objective_general_basis(lpg):
     assert res.status == ores.status and res.objective == ores.objective
 
 
-@pytest.mark.parametrize("variant", list(range(14)))
+@pytest.mark.parametrize("variant", list(range(20)))
 def test_update_variants_identical(lpg, variant, monkeypatch):
     monkeypatch.setenv("LPG_UPDATE_VARIANT", str(variant))
     m, n = 300, 700
@@ -244,6 +244,27 @@ def test_column_skipping_is_value_identical(lpg, m, n, kind, rule, piv, monkeypa
     # 16-byte slices: an odd N+1 rounds up to one padding double per row
     assert tf.update_bytes == tf.update_count * 32 * (m + 1) * ((n + m + 2) // 2)
     assert 0 < te.update_bytes < tf.update_bytes
+
+
+def test_graph_replay_identical(lpg, monkeypatch):
+    """Batches of >= 64 pivots replay a captured hipGraph of 32 pivots; the result
+    must be bitwise the eager launches (LPG_NO_GRAPH=1) and the oracle."""
+    m, n = 200, 300
+    e = lpg.Engine(m, n + m + 1)
+    monkeypatch.setenv("LPG_NO_GRAPH", "1")
+    f = lpg.Engine(m, n + m + 1)
+    monkeypatch.delenv("LPG_NO_GRAPH")
+    o = Oracle(m, n + m + 1)
+    for x in (e, f, o):
+        x.generate(n, 61, 0)
+    e.enqueue(1, 0)            # odd start: the graph path must realign to parity 0
+    e.enqueue(150, 0)
+    r = e.sync()
+    f.solve(151, 0)
+    o.solve(151, 0)
+    assert r.pivots == o.get_log()[0].size
+    _assert_same(e, o, m)
+    _assert_same(f, o, m)
 
 
 def test_timing_counters(lpg):
