@@ -185,8 +185,16 @@ def main():
     # that hides its launch overhead, so config 2 times the update kernel in a
     # second, event-instrumented pass right after the timed region.
     live_events = a.config != 2
+    if not live_events:                                # config 2: event-instrumented pass first, while the LP
+        eng.set_timing(True)                           # is far from optimal, then the graph-replayed timed region
+        eng.get_timing()
+        eng.enqueue(100, lpg.RULE_DANTZIG)
+        eng.sync()
+        timing = eng.get_timing()
+        before = eng.sync().pivots
     eng.set_timing(live_events)
-    eng.get_timing()                                   # reset sums
+    if live_events:
+        eng.get_timing()                               # reset sums
     if world > 1:
         dist.barrier()
     eng.device_sync()
@@ -198,12 +206,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    timing = eng.get_timing()
-    if not live_events:
-        eng.set_timing(True)
-        eng.get_timing()
-        eng.enqueue(min(a.steps, 100), lpg.RULE_DANTZIG)
-        eng.sync()
+    if live_events:
         timing = eng.get_timing()
     info = eng.info
     if world > 1:

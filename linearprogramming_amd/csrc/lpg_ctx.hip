@@ -354,9 +354,12 @@ static int reset_state(lpg_ctx *c) {
     return 0;
 }
 
+static void graph_drop(lpg_ctx *c);
+
 static int ensure_log(lpg_ctx *c, int64_t need) {
     if (c->flags & LPG_FLAG_NO_LOG) return 0;
     if (need <= c->logcap) return 0;
+    graph_drop(c);   // a captured graph holds the old log pointers
     int64_t cap = std::max<int64_t>(need, 2 * c->logcap);
     int64_t *nk = nullptr, *nr = nullptr;
     HIPCHK(c, hipStreamSynchronize(c->stream));

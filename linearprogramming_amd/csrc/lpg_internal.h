@@ -35,6 +35,7 @@ struct DevState {
     int64_t last_k, last_r;
     int64_t logcap;
     unsigned long long touched;   // 16-byte slices the update read+wrote (column skipping accounting)
+    unsigned long long work[2];   // k_update work-item dequeue heads, per pivot parity (reset by k_prep)
 };
 
 // Ratio-test candidate: lexicographic (theta, key); row < 0 = none.

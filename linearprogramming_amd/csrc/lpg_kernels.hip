@@ -313,7 +313,10 @@ __global__ __launch_bounds__(kBlock) void k_prep(const double *__restrict__ T, G
         }
         return;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->slot[s].r = best.row;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->slot[s].r = best.row;
+        st->work[s] = 0;   // k_update's dequeue head for this pivot (runs after this kernel)
+    }
     const int64_t rl = best.row - g.row0;
     const bool own = rl >= 0 && rl < g.nloc;
     const double piv = best.piv;   // == T_t[r][k_t] (select_{t-1} computed and stored it)
@@ -523,7 +526,7 @@ __device__ __forceinline__ void upd_compute_store(d2 (&t)[RU][VPT], d2 *__restri
             }
 }
 
-template <int VPT, int RU, bool NT, bool PIPE>
+template <int VPT, int RU, bool NT, bool PIPE, bool DYN>
 __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g, DevState *__restrict__ st, int s,
                                                    const double *__restrict__ P, const double *__restrict__ Cs,
                                                    int64_t ntiles, int64_t strip_rows, int64_t nitems,
@@ -541,7 +544,16 @@ __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g
     d2 *__restrict__ Tv = (d2 *)T;
     const d2 *__restrict__ Pv = (const d2 *)P;
 
-    for (int64_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+    __shared__ int64_t next_item;
+    for (int64_t item = DYN ? -1 : blockIdx.x;; item += DYN ? 0 : gridDim.x) {
+        if (DYN) {
+            // dynamic balance: one device-scope dequeue per 4*VPT KB x SR-row item
+            __syncthreads();
+            if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->work[s], 1ull);
+            __syncthreads();
+            item = next_item;
+        }
+        if (item >= nitems) break;
         const int64_t tile = item % ntiles;
         const int64_t strip = item / ntiles;
         const int64_t i0 = strip * strip_rows;
@@ -646,6 +658,11 @@ static const UpdateCfg kUpdateCfgs[] = {
     {1, 8, true, true, 64, 8},      // 17 persistent + non-temporal + pipelined
     {1, 8, false, false, 32, 8},    // 18 persistent, 32-row strips
     {1, 8, true, false, 32, 8},     // 19 persistent + non-temporal, 32-row strips
+    {1, 8, true, false, 64, 8},     // 20 persistent + non-temporal, dynamic dequeue
+    {1, 8, true, true, 64, 8},      // 21 persistent + non-temporal + pipelined, dynamic dequeue
+    {1, 8, false, false, 64, 8},    // 22 persistent, dynamic dequeue
+    {2, 4, true, false, 64, 8},     // 23 2 slices/lane, persistent + non-temporal, dynamic
+    {1, 8, true, false, 64, 4},     // 24 persistent 4/CU + non-temporal, dynamic
 };
 constexpr int kNumUpdateCfgs = sizeof(kUpdateCfgs) / sizeof(kUpdateCfgs[0]);
 
@@ -669,9 +686,10 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
     if (nblocks > 0x7fffffff) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
     dim3 grid((unsigned)nblocks), blk(kBlock);
-#define LPG_UPD(V, R, N, PI)                                                                                  \
-    hipLaunchKernelGGL((k_update<V, R, N, PI>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, ntiles, strip,    \
+#define LPG_UPD_(V, R, N, PI, D)                                                                              \
+    hipLaunchKernelGGL((k_update<V, R, N, PI, D>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, ntiles, strip, \
                        nitems, basis, logk, logr, skip)
+#define LPG_UPD(V, R, N, PI) LPG_UPD_(V, R, N, PI, false)
     switch (variant) {
         case 1: LPG_UPD(2, 4, false, false); break;
         case 2: LPG_UPD(1, 8, true, false); break;
@@ -692,9 +710,15 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
         case 17: LPG_UPD(1, 8, true, true); break;
         case 18: LPG_UPD(1, 8, false, false); break;
         case 19: LPG_UPD(1, 8, true, false); break;
+        case 20: LPG_UPD_(1, 8, true, false, true); break;
+        case 21: LPG_UPD_(1, 8, true, true, true); break;
+        case 22: LPG_UPD_(1, 8, false, false, true); break;
+        case 23: LPG_UPD_(2, 4, true, false, true); break;
+        case 24: LPG_UPD_(1, 8, true, false, true); break;
         default: LPG_UPD(1, 8, false, false); break;
     }
 #undef LPG_UPD
+#undef LPG_UPD_
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -211,7 +211,7 @@ def test_set_objective_general_basis(lpg):
     assert res.status == ores.status and res.objective == ores.objective
 
 
-@pytest.mark.parametrize("variant", list(range(20)))
+@pytest.mark.parametrize("variant", list(range(25)))
 def test_update_variants_identical(lpg, variant, monkeypatch):
     monkeypatch.setenv("LPG_UPDATE_VARIANT", str(variant))
     m, n = 300, 700

@@ -25,7 +25,7 @@ ap.add_argument("--variants", default="")
 a = ap.parse_args()
 m, n = CONFIGS[a.config]
 lib = lpg.load()
-nvar = 20
+nvar = 25
 variants = [int(v) for v in a.variants.split(",")] if a.variants else list(range(nvar))
 res = {v: [] for v in variants}
 logs = {}
