@@ -49,6 +49,7 @@ struct lpg_ctx {
     double *cb = nullptr;         // nloc
     double *cost = nullptr;       // ncols
     PricePart *pp = nullptr;
+    int *pc = nullptr;            // npp live-slice counts of P (column-skipping accounting)
     Cand *part = nullptr;         // nsel (this rank's select partials)
     Cand *cand = nullptr;         // world * nsel (gathered); == part when world == 1
     int64_t *basis = nullptr;     // m (replicated)
@@ -207,10 +208,10 @@ static int exchange_candidates(lpg_ctx *c) {
 static int bootstrap(lpg_ctx *c, int rule) {
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
     const Geo g = geo(c);
-    if (launch_price(lau(c), g, rule, 0, c->st, 0, c->P, c->C[0], c->pp, c->npp))
+    if (launch_price(lau(c), g, rule, 0, c->st, 0, c->P, c->C[0], c->pp, c->pc, c->npp))
         return fail(c, LPG_ERR_DEVICE, "price launch failed");
     if (launch_select(lau(c), g, rule, true, c->st, 0, 0, c->P, c->C[1], c->C[0], c->pp, c->npp, c->basis,
-                      c->part, c->nsel))
+                      c->part, c->nsel, 0, -1, c->pc, c->skip))
         return fail(c, LPG_ERR_DEVICE, "select launch failed");
     int rc = exchange_candidates(c);
     if (rc) return rc;
@@ -225,7 +226,7 @@ static int bootstrap(lpg_ctx *c, int rule) {
 static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
     if (launch_select(lau(c), geo(c), rule, true, c->st, 0, 0, c->P, c->C[1], c->C[0], c->pp, c->npp, c->basis,
-                      c->part, c->nsel, k, r))
+                      c->part, c->nsel, k, r, c->pc, c->skip))
         return fail(c, LPG_ERR_DEVICE, "select launch failed");
     int rc = exchange_candidates(c);
     if (rc) return rc;
@@ -301,15 +302,15 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
         const int s = c->par, s1 = s ^ 1;
         int rc;
         if (c->timing && (rc = timing_mark(c, 0))) return rc;
-        if (launch_prep(L, g, rule, fuse, c->st, s, c->cand, ncand, c->P, c->C[s], c->pp, c->npp))
+        if (launch_prep(L, g, rule, fuse, c->st, s, c->cand, ncand, c->P, c->C[s], c->pp, c->pc, c->npp))
             return fail(c, LPG_ERR_DEVICE, "prep launch failed");
         if (!fuse) {
             if ((rc = comm_allreduce_sum(c, c->P, (size_t)c->ld))) return rc;
-            if (launch_price(L, g, rule, 1, c->st, s, c->P, c->C[s], c->pp, c->npp))
+            if (launch_price(L, g, rule, 1, c->st, s, c->P, c->C[s], c->pp, c->pc, c->npp))
                 return fail(c, LPG_ERR_DEVICE, "price launch failed");
         }
         if (launch_select(L, g, rule, false, c->st, s, s1, c->P, c->C[s], c->C[s1], c->pp, c->npp, c->basis,
-                          c->part, c->nsel))
+                          c->part, c->nsel, 0, -1, c->pc, c->skip))
             return fail(c, LPG_ERR_DEVICE, "select launch failed");
         if ((rc = exchange_candidates(c))) return rc;
         if (c->timing && (rc = timing_mark(c, 1))) return rc;
@@ -450,6 +451,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     ALLOC(c->cb, (size_t)std::max<int64_t>(c->nloc, 1) * sizeof(double));
     ALLOC(c->cost, (size_t)ncols * sizeof(double));
     ALLOC(c->pp, (size_t)c->npp * sizeof(PricePart));
+    ALLOC(c->pc, (size_t)c->npp * sizeof(int));
     ALLOC(c->part, (size_t)c->nsel * sizeof(Cand));
     if (world > 1) ALLOC(c->cand, (size_t)c->nsel * world * sizeof(Cand));
     else c->cand = c->part;
@@ -522,7 +524,7 @@ void lpg_destroy(lpg_ctx *c) {
     if (c->nccl) ncclCommDestroy(c->nccl);
     for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
-    void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->part, c->basis, c->logk, c->logr, c->st};
+    void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);

@@ -74,12 +74,13 @@ int launch_generate(const Launch &L, const Geo &g, int64_t n, uint64_t seed, int
 int launch_objective_chain(const Launch &L, const Geo &g, const double *cb, const double *acc_in, double *acc_out);
 int launch_objective_finish(const Launch &L, const Geo &g, const double *acc, const double *cost);
 int launch_price(const Launch &L, const Geo &g, int rule, int mode, const DevState *st, int s,
-                 const double *P, const double *Cs, PricePart *pp, int npp);
+                 const double *P, const double *Cs, PricePart *pp, int *pc, int npp);
 int launch_prep(const Launch &L, const Geo &g, int rule, bool fuse_price, DevState *st, int s,
-                const Cand *cand, int ncand, double *P, const double *Cs, PricePart *pp, int npp);
+                const Cand *cand, int ncand, double *P, const double *Cs, PricePart *pp, int *pc, int npp);
 int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState *st, int s, int s1,
                   const double *P, const double *Cs, double *Cs1, const PricePart *pp, int npp,
-                  const int64_t *basis, Cand *part, int nsel, int64_t force_k = 0, int64_t force_r = -1);
+                  const int64_t *basis, Cand *part, int nsel, int64_t force_k, int64_t force_r,
+                  const int *pc, int skip);
 int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
                   int64_t *basis, int64_t *logk, int64_t *logr, int variant, int skip);
 

@@ -249,15 +249,23 @@ int price_blocks(const Geo &g) {
     return (int)((nvec + kBlock - 1) / kBlock);
 }
 
+// Number of 16-byte slices of P that are not all zero (the slices k_update
+// will read and write): per-block counts, summed once per pivot by k_select.
+__device__ __forceinline__ void count_live(int *__restrict__ pc, bool live) {
+    const int n = __syncthreads_count(live);
+    if (threadIdx.x == 0) pc[blockIdx.x] = n;
+}
+
 template <int RULE, int MODE>
 __global__ __launch_bounds__(kBlock) void k_price(const double *__restrict__ T, Geo g,
                                                   const DevState *__restrict__ st, int s,
                                                   const double *__restrict__ P, const double *__restrict__ Cs,
-                                                  PricePart *__restrict__ pp) {
+                                                  PricePart *__restrict__ pp, int *__restrict__ pc) {
     if (MODE == 1 && st->slot[s].status != RUNNING) return;
     const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t nvec = (g.ncols + 1) / 2;
     PricePart best{0.0, -1};
+    bool live = false;
     if (j2 < nvec) {
         const d2 d = *(const d2 *)(T + g.nloc * g.ld + 2 * j2);
         d2 dn = d;
@@ -266,24 +274,26 @@ __global__ __launch_bounds__(kBlock) void k_price(const double *__restrict__ T, 
             const d2 p = *(const d2 *)(P + 2 * j2);
             dn.x = fma(c, p.x, d.x);
             dn.y = fma(c, p.y, d.y);
+            live = p.x != 0.0 || p.y != 0.0;
         }
         price_one<RULE>(best, dn.x, 2 * j2, g);
         price_one<RULE>(best, dn.y, 2 * j2 + 1, g);
     }
+    if (MODE == 1) count_live(pc, live);
     best = block_reduce_pp<RULE>(best);
     if (threadIdx.x == 0) pp[blockIdx.x] = best;
 }
 
 int launch_price(const Launch &L, const Geo &g, int rule, int mode, const DevState *st, int s,
-                 const double *P, const double *Cs, PricePart *pp, int npp) {
+                 const double *P, const double *Cs, PricePart *pp, int *pc, int npp) {
     hipStream_t stream = (hipStream_t)L.stream;
     dim3 grid(npp), blk(kBlock);
     if (rule == RULE_BLAND) {
-        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_BLAND, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp);
-        else hipLaunchKernelGGL((k_price<RULE_BLAND, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp);
+        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_BLAND, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc);
+        else hipLaunchKernelGGL((k_price<RULE_BLAND, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc);
     } else {
-        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_DANTZIG, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp);
-        else hipLaunchKernelGGL((k_price<RULE_DANTZIG, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp);
+        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_DANTZIG, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc);
+        else hipLaunchKernelGGL((k_price<RULE_DANTZIG, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -298,7 +308,7 @@ template <int RULE, bool FUSE>
 __global__ __launch_bounds__(kBlock) void k_prep(const double *__restrict__ T, Geo g, DevState *st, int s,
                                                  const Cand *__restrict__ cand, int ncand,
                                                  double *__restrict__ P, const double *__restrict__ Cs,
-                                                 PricePart *__restrict__ pp) {
+                                                 PricePart *__restrict__ pp, int *__restrict__ pc) {
     if (st->slot[s].status != RUNNING) return;
     Cand best{0.0, 0.0, 0, -1};
     for (int q = threadIdx.x; q < ncand; q += kBlock) {
@@ -324,6 +334,7 @@ __global__ __launch_bounds__(kBlock) void k_prep(const double *__restrict__ T, G
     const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t nvec = (g.ncols + 1) / 2;
     PricePart pbest{0.0, -1};
+    bool live = false;
     if (j2 < nvec) {
         d2 p = d2{0.0, 0.0};
         if (own) {
@@ -337,24 +348,26 @@ __global__ __launch_bounds__(kBlock) void k_prep(const double *__restrict__ T, G
             const double c = -Cs[g.nloc];
             price_one<RULE>(pbest, fma(c, p.x, d.x), 2 * j2, g);
             price_one<RULE>(pbest, fma(c, p.y, d.y), 2 * j2 + 1, g);
+            live = p.x != 0.0 || p.y != 0.0;
         }
     }
     if (FUSE) {
+        count_live(pc, live);
         pbest = block_reduce_pp<RULE>(pbest);
         if (threadIdx.x == 0) pp[blockIdx.x] = pbest;
     }
 }
 
 int launch_prep(const Launch &L, const Geo &g, int rule, bool fuse, DevState *st, int s, const Cand *cand,
-                int ncand, double *P, const double *Cs, PricePart *pp, int npp) {
+                int ncand, double *P, const double *Cs, PricePart *pp, int *pc, int npp) {
     hipStream_t stream = (hipStream_t)L.stream;
     dim3 grid(npp), blk(kBlock);
     if (rule == RULE_BLAND) {
-        if (fuse) hipLaunchKernelGGL((k_prep<RULE_BLAND, true>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp);
-        else hipLaunchKernelGGL((k_prep<RULE_BLAND, false>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp);
+        if (fuse) hipLaunchKernelGGL((k_prep<RULE_BLAND, true>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp, pc);
+        else hipLaunchKernelGGL((k_prep<RULE_BLAND, false>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp, pc);
     } else {
-        if (fuse) hipLaunchKernelGGL((k_prep<RULE_DANTZIG, true>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp);
-        else hipLaunchKernelGGL((k_prep<RULE_DANTZIG, false>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp);
+        if (fuse) hipLaunchKernelGGL((k_prep<RULE_DANTZIG, true>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp, pc);
+        else hipLaunchKernelGGL((k_prep<RULE_DANTZIG, false>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp, pc);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -373,7 +386,8 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
                                                    const double *__restrict__ Cs, double *__restrict__ Cs1,
                                                    const PricePart *__restrict__ pp, int npp,
                                                    const int64_t *__restrict__ basis, Cand *__restrict__ part,
-                                                   int64_t force_k, int64_t force_r) {
+                                                   int64_t force_k, int64_t force_r,
+                                                   const int *__restrict__ pc, int skip) {
     Slot *dst = &st->slot[s1];
     if (!FIRST) {
         const int32_t stt = st->slot[s].status;
@@ -384,6 +398,26 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
                 dst->r = -1;
             }
             return;
+        }
+    }
+    if (!FIRST && blockIdx.x == 0) {
+        // the update of this pivot (next on the stream) touches the live
+        // slices of P (all slices without column skipping) in every row
+        const int64_t nvec = (g.ncols + 1) / 2;
+        int64_t live = 0;
+        if (skip)
+            for (int q = threadIdx.x; q < npp; q += kBlock) live += pc[q];
+        else if (threadIdx.x == 0)
+            live = nvec;
+#pragma unroll
+        for (int mask = 32; mask > 0; mask >>= 1) live += __shfl_xor((long long)live, mask, 64);
+        __shared__ int64_t wsum[kBlock / 64];
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = live;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t tot = 0;
+            for (int w = 0; w < kBlock / 64; w++) tot += wsum[w];
+            st->touched += (unsigned long long)tot * (unsigned long long)(g.nloc + g.nobj);
         }
     }
     PricePart pb{0.0, -1};
@@ -455,12 +489,12 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
 
 int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState *st, int s, int s1, const double *P,
                   const double *Cs, double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part,
-                  int nsel, int64_t force_k, int64_t force_r) {
+                  int nsel, int64_t force_k, int64_t force_r, const int *pc, int skip) {
     hipStream_t stream = (hipStream_t)L.stream;
     dim3 grid(nsel), blk(kBlock);
 #define LPG_SEL(R, F)                                                                                     \
     hipLaunchKernelGGL((k_select<R, F>), grid, blk, 0, stream, g.T, g, st, s, s1, P, Cs, Cs1, pp, npp, basis, \
-                       part, force_k, force_r)
+                       part, force_k, force_r, pc, skip)
     if (rule == RULE_BLAND) {
         if (first) LPG_SEL(RULE_BLAND, true); else LPG_SEL(RULE_BLAND, false);
     } else {
@@ -561,7 +595,7 @@ __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g
         const int64_t cb = tile * (kBlock * VPT) + threadIdx.x;
         d2 p[VPT];
         bool ok[VPT];
-        int live = 0;
+        int live = 0;   // slices this lane still updates
 #pragma unroll
         for (int v = 0; v < VPT; v++) {
             ok[v] = cb + v * kBlock < nvec;
@@ -574,7 +608,6 @@ __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g
             if (skip && p[v].x == 0.0 && p[v].y == 0.0) ok[v] = false;
             live += ok[v] ? 1 : 0;
         }
-        const int64_t i0c = i0, i1c = i1;
         // a tile whose pivot-row slice is all zero is skipped as a whole
         if (skip && !__syncthreads_or(live)) continue;
         int64_t i = i0;
@@ -607,12 +640,6 @@ __global__ __launch_bounds__(kBlock) void k_update(double *__restrict__ T, Geo g
             upd_load<VPT, 1, NT>(t, Tv, i, ld2, cb, ok);
             upd_compute_store<VPT, 1, NT>(t, Tv, i, ld2, cb, ok, p, Cs, rl);
         }
-        // touched-bytes accounting: one 64-bit atomic per work item
-        int wl = live;
-#pragma unroll
-        for (int mask = 32; mask > 0; mask >>= 1) wl += __shfl_xor(wl, mask, 64);
-        if ((threadIdx.x & 63) == 0 && wl)
-            atomicAdd(&st->touched, (unsigned long long)wl * (unsigned long long)(i1c - i0c));
     }
 
     if (blockIdx.x == 0 && threadIdx.x == 0) {
