@@ -241,7 +241,7 @@ def main():
                    "tableau_GB": (m + 1) * (n + m + 1) * 8 / 1e9, "rule": "dantzig",
                    "parallelism": f"row-block x{world}" + (" (RCCL allgather + allreduce per pivot)"
                                                            if world > 1 or a.force_rccl else ""),
-                   "update_variant": int(os.environ.get("LPG_UPDATE_VARIANT", "0"))},
+                   "update_variant": int(os.environ.get("LPG_UPDATE_VARIANT", "-1"))},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "lpg::k_update (Gauss-Jordan rank-1)",

@@ -421,7 +421,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->nact = ncols - 1;
     c->flags = flags;
     const char *uv = getenv("LPG_UPDATE_VARIANT");
-    c->update_variant = uv ? atoi(uv) : 0;
+    c->update_variant = uv ? atoi(uv) : -1;   // -1: size-adaptive default (launch_update)
     const char *ng = getenv("LPG_NO_GRAPH");
     c->use_graphs = !(ng && atoi(ng));
     const char *ns = getenv("LPG_NO_SKIP");

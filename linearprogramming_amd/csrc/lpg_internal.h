@@ -86,5 +86,6 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
 
 int price_blocks(const Geo &g);      // number of pricing partials (= prep / price grid)
 int update_variants();               // entries of the update-kernel variant table
+int update_auto_variant(const Geo &g);   // default variant for this geometry
 
 }  // namespace lpg
