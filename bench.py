@@ -100,11 +100,6 @@ def config5(a):
     eng.device_sync()
     elapsed = time.perf_counter() - t0
     timing = eng.get_timing()
-    done = res.pivots - before          # pivots really applied (an LP that finishes early turns the rest into no-ops)
-    if world > 1:
-        dd = torch.tensor([done], dtype=torch.int64)
-        dist.all_reduce(dd, op=dist.ReduceOp.MIN)
-        done = int(dd.item())
     upd_ms = timing.update_ms / max(timing.update_count, 1)
     touched = timing.update_bytes / max(timing.update_count, 1)
     achieved = touched / (upd_ms * 1e-3) / 1e9 if upd_ms > 0 else 0.0

@@ -16,6 +16,7 @@
  * Tableau layout (row-major fp64, same as SimplexMatrix.cMatrix flattened):
  *   rows 0..m-1  constraint rows  [b_i | a_i1 .. a_iN]   (matrix.c:42-48, 62-66)
  *   row  m       objective row    [z   | d_1  .. d_N ]   d_j = z_j - c_j
+ *   (LPG_FLAG_BIG_M: row m = M part, row m+1 = real part; d_j = dM_j M + dR_j)
  *   columns      0 = b, 1..N = variables in LPAlign order (simplex.c:238-260)
  * The reference maximises (LPStandardize turns min into max, simplex.c:99-106),
  * so the engine maximises; the optimum is reached when every d_j >= -eps_opt.
@@ -72,6 +73,7 @@ extern "C" {
 /* ---- lpg_create flags ---- */
 #define LPG_FLAG_NO_LOG  0x1u  /* do not record the (entering, leaving) pivot log */
 #define LPG_FLAG_NO_SKIP 0x2u  /* update every column (no skipping of P[j] == 0 slices) */
+#define LPG_FLAG_BIG_M   0x4u  /* two objective rows: row m = M part, row m+1 = real part (Big-M) */
 
 typedef struct lpg_ctx lpg_ctx;
 
@@ -145,6 +147,9 @@ int  lpg_set_basis(lpg_ctx *ctx, const int64_t *basis);
  * SimplexMatrix.ofCosts / basicCosts (matrix.c:55-57, 76-77). The pivot
  * count and log are kept (phase I -> phase II). */
 int  lpg_set_objective(lpg_ctx *ctx, const double *c);
+/* Big-M contexts: the M-part objective row from M-part costs (the real row
+ * comes from lpg_set_objective). */
+int  lpg_set_objective_m(lpg_ctx *ctx, const double *costM);
 int  lpg_set_tolerances(lpg_ctx *ctx, double eps_piv, double eps_opt);
 /* Price only columns 1..nact (e.g. to exclude artificials). */
 int  lpg_set_active_columns(lpg_ctx *ctx, int64_t nact);
@@ -180,6 +185,16 @@ int  lpg_pivot(lpg_ctx *ctx, int64_t k, int64_t r);
  * Single rank. */
 int  lpg_solve_two_phase(lpg_ctx *ctx, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
                          lpg_result *out);
+
+/* Big-M method (reference: the empty `case 1:` of simplex.c:58-60, constant
+ * M of dataReader.c:165-173) on a LPG_FLAG_BIG_M context: artificial columns
+ * art_first..N cost -M, kept symbolic as a second objective row, so pricing
+ * is lexicographic (M part first) exactly like the reference's Number with a
+ * constant (numOprts.h:15-37); no numeric M is ever formed. An optimum with a
+ * negative M part means LPG_INFEASIBLE. cost NULL: -1 x the real objective
+ * row as loaded. */
+int  lpg_solve_big_m(lpg_ctx *ctx, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
+                     lpg_result *out);
 
 /* ---- readout ---- */
 int  lpg_get_rows(lpg_ctx *ctx, int64_t row0, int64_t nrows, double *out, int64_t ld);

@@ -21,6 +21,7 @@ RULE_DANTZIG, RULE_BLAND = 0, 1
 GEN_DENSE, GEN_DEGENERATE, GEN_ARTIFICIAL = 0, 1, 2
 FLAG_NO_LOG = 0x1
 FLAG_NO_SKIP = 0x2
+FLAG_BIG_M = 0x4
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int64_p = ctypes.POINTER(ctypes.c_int64)
@@ -67,6 +68,7 @@ PROTOTYPES = [
     ("lpg_load_rows", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, c_double_p, ctypes.c_int64]),
     ("lpg_set_basis", ctypes.c_int, [ctypes.c_void_p, c_int64_p]),
     ("lpg_set_objective", ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    ("lpg_set_objective_m", ctypes.c_int, [ctypes.c_void_p, c_double_p]),
     ("lpg_set_tolerances", ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_double]),
     ("lpg_set_active_columns", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     ("lpg_generate", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int]),
@@ -77,6 +79,8 @@ PROTOTYPES = [
     ("lpg_pivot", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]),
     ("lpg_solve_two_phase", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, c_double_p, ctypes.c_int64, ctypes.c_int,
                                            ctypes.POINTER(Result)]),
+    ("lpg_solve_big_m", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, c_double_p, ctypes.c_int64, ctypes.c_int,
+                                       ctypes.POINTER(Result)]),
     ("lpg_get_rows", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, c_double_p, ctypes.c_int64]),
     ("lpg_get_basis", ctypes.c_int, [ctypes.c_void_p, c_int64_p]),
     ("lpg_get_column0", ctypes.c_int, [ctypes.c_void_p, c_double_p]),

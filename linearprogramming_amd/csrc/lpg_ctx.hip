@@ -327,7 +327,7 @@ static int read_result(lpg_ctx *c, lpg_result *out, int rule) {
     DevState h;
     HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));
     double z = 0;
-    HIPCHK(c, hipMemcpyAsync(&z, c->T + c->nloc * c->ld, sizeof z, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&z, c->T + (c->nloc + c->nobj - 1) * c->ld, sizeof z, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (out) {
         const int32_t s = c->booted ? h.slot[c->par].status : RUNNING;
@@ -416,6 +416,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->m = m;
     c->ncols = ncols;
     c->ld = (ncols + 63) & ~(int64_t)63;   // 512-byte aligned rows
+    c->nobj = (flags & LPG_FLAG_BIG_M) ? 2 : 1;
     c->row0 = m * rank / world;
     c->nloc = m * (rank + 1) / world - c->row0;
     c->nact = ncols - 1;
@@ -576,8 +577,20 @@ int lpg_set_basis(lpg_ctx *c, const int64_t *basis) {
     return reset_state(c);
 }
 
+static int set_objective_row(lpg_ctx *c, const double *cost, int64_t orow);
+
 int lpg_set_objective(lpg_ctx *c, const double *cost) {
     if (!c || !cost) return fail(c, LPG_ERR_ARG, "cost is NULL");
+    return set_objective_row(c, cost, c->nloc + c->nobj - 1);
+}
+
+int lpg_set_objective_m(lpg_ctx *c, const double *costM) {
+    if (!c || !costM) return fail(c, LPG_ERR_ARG, "cost is NULL");
+    if (c->nobj != 2) return fail(c, LPG_ERR_STATE, "lpg_set_objective_m needs a context created with LPG_FLAG_BIG_M");
+    return set_objective_row(c, costM, c->nloc);
+}
+
+static int set_objective_row(lpg_ctx *c, const double *cost, int64_t orow) {
     int rc;
     if ((rc = use_device(c))) return rc;
     std::vector<int64_t> hb(c->m);
@@ -603,7 +616,8 @@ int lpg_set_objective(lpg_ctx *c, const double *cost) {
         }
         if ((rc = comm_allreduce_sum(c, chain, (size_t)c->ncols))) return rc;
     }
-    if (launch_objective_finish(lau(c), g, chain, c->cost)) return fail(c, LPG_ERR_DEVICE, "objective finish failed");
+    if (launch_objective_finish(lau(c), g, chain, c->cost, orow))
+        return fail(c, LPG_ERR_DEVICE, "objective finish failed");
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->booted = false;   // re-price from the new objective row; the pivot count and log carry on
     return 0;
@@ -763,6 +777,43 @@ int lpg_solve_two_phase(lpg_ctx *c, int64_t art_first, const double *cost, int64
     lpg_result r2;
     if ((rc = lpg_solve(c, std::max<int64_t>(max_pivots - used, 0), rule, &r2))) return rc;
     if (out) *out = r2;
+    return 0;
+}
+
+int lpg_solve_big_m(lpg_ctx *c, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
+                    lpg_result *out) {
+    if (!c || art_first < 2 || art_first >= c->ncols || max_pivots < 0)
+        return fail(c, LPG_ERR_ARG, "lpg_solve_big_m: bad arguments");
+    if (c->nobj != 2) return fail(c, LPG_ERR_STATE, "lpg_solve_big_m needs a context created with LPG_FLAG_BIG_M");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    const int64_t N = c->ncols - 1;
+    std::vector<double> cr(N), cm(N, 0.0), row(c->ncols);
+    if (cost) {
+        for (int64_t j = 0; j < N; j++) cr[j] = cost[j];
+    } else {   // costs = -1 x the (real) objective row as loaded (slack-form -c row)
+        if ((rc = lpg_get_rows(c, c->m + c->nobj - 1, 1, row.data(), c->ncols))) return rc;
+        for (int64_t j = 1; j <= N; j++) cr[j - 1] = -row[j];
+    }
+    for (int64_t j = art_first; j <= N; j++) {   // artificial: cost -M (max form) = M part -1, real part 0
+        cr[j - 1] = 0.0;
+        cm[j - 1] = -1.0;
+    }
+    if ((rc = lpg_set_active_columns(c, N)) || (rc = lpg_set_objective_m(c, cm.data())) ||
+        (rc = lpg_set_objective(c, cr.data())))
+        return rc;
+    lpg_result r;
+    if ((rc = lpg_solve(c, max_pivots, rule, &r))) return rc;
+    if (r.status == LPG_OPTIMAL) {
+        // artificials still positive (M-part objective < 0) -> infeasible
+        double zM = 0, bsum = 0;
+        std::vector<double> xb(c->nloc);
+        if ((rc = lpg_get_rows(c, c->m, 1, row.data(), c->ncols)) || (rc = lpg_get_column0(c, xb.data()))) return rc;
+        zM = row[0];
+        for (double v : xb) bsum += fabs(v);
+        if (zM < -1e-9 * std::max(1.0, bsum)) r.status = LPG_INFEASIBLE;
+    }
+    if (out) *out = r;
     return 0;
 }
 

@@ -46,10 +46,15 @@ struct Cand {                 // 32 B
     int64_t row;              // global row
 };
 
-// Pricing partial: Dantzig (v, j) lexicographic; Bland smallest eligible j.
-struct PricePart {            // 16 B
+// Pricing partial of an eligible column: Dantzig (cls, v, j) lexicographic,
+// Bland smallest j. One objective row: cls 0, v = d_j < -eps. Big-M (two
+// objective rows, M part first): cls 0 if dM_j < -eps (v = dM_j); cls 1 if
+// |dM_j| <= eps and dR_j < -eps (v = dR_j), i.e. d_j = dM_j M + dR_j < 0.
+struct PricePart {            // 24 B
     double  v;
     int64_t j;                // -1 = none
+    int32_t cls;
+    int32_t pad;
 };
 
 // Geometry of this rank's slice of the tableau.
@@ -72,7 +77,7 @@ struct Launch {
 
 int launch_generate(const Launch &L, const Geo &g, int64_t n, uint64_t seed, int kind, int64_t *basis_dev);
 int launch_objective_chain(const Launch &L, const Geo &g, const double *cb, const double *acc_in, double *acc_out);
-int launch_objective_finish(const Launch &L, const Geo &g, const double *acc, const double *cost);
+int launch_objective_finish(const Launch &L, const Geo &g, const double *acc, const double *cost, int64_t orow);
 int launch_price(const Launch &L, const Geo &g, int rule, int mode, const DevState *st, int s,
                  const double *P, const double *Cs, PricePart *pp, int *pc, int npp);
 int launch_prep(const Launch &L, const Geo &g, int rule, bool fuse_price, DevState *st, int s,

@@ -37,6 +37,7 @@ __device__ __forceinline__ bool pp_better(const PricePart &a, const PricePart &b
     if (a.j < 0) return false;
     if (b.j < 0) return true;
     if (RULE == RULE_BLAND) return a.j < b.j;
+    if (a.cls != b.cls) return a.cls < b.cls;
     if (a.v != b.v) return a.v < b.v;
     return a.j < b.j;
 }
@@ -54,6 +55,8 @@ __device__ __forceinline__ PricePart shfl_xor_pp(const PricePart &p, int mask) {
     PricePart o;
     o.v = __shfl_xor(p.v, mask, 64);
     o.j = __shfl_xor((long long)p.j, mask, 64);
+    o.cls = __shfl_xor(p.cls, mask, 64);
+    o.pad = 0;
     return o;
 }
 
@@ -95,17 +98,27 @@ __device__ PricePart block_reduce_pp(PricePart p) {
     return b;
 }
 
-// Pricing candidate of one reduced cost d_j.
+// Pricing candidate of column j: dR is the (real)
+// objective row entry; with Big-M (g.nobj == 2) dM is the M-part entry and the
+// comparison is lexicographic (M part first). NaN entries are never eligible.
 template <int RULE>
-__device__ __forceinline__ void price_one(PricePart &best, double d, int64_t j, const Geo &g) {
+__device__ __forceinline__ void price_one(PricePart &best, double dM, double dR, int64_t j, const Geo &g) {
     if (j < 1 || j > g.nact) return;
     PricePart c;
-    c.v = d;
     c.j = j;
-    if (RULE == RULE_BLAND) {
-        if (!(d < -g.eps_opt)) return;
+    c.pad = 0;
+    if (g.nobj == 1) {
+        if (!(dR < -g.eps_opt)) return;
+        c.cls = 0;
+        c.v = dR;
+    } else if (dM < -g.eps_opt) {
+        c.cls = 0;
+        c.v = dM;
+    } else if (dM <= g.eps_opt && dR < -g.eps_opt) {
+        c.cls = 1;
+        c.v = dR;
     } else {
-        if (!(d == d)) return;   // NaN never wins
+        return;
     }
     if (pp_better<RULE>(c, best)) best = c;
 }
@@ -174,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_generate(double *__restrict__ T, Geo
             } else if (j == unit_column(g.m, n, gi, kind)) {
                 x = 1.0;
             }
-        } else if (i == g.nloc) {
+        } else if (i == g.nloc + g.nobj - 1) {   // (real) objective row; a Big-M M row stays zero
             if (j >= 1 && j <= n) x = -(1.0 + uniform01(kC, (uint64_t)(j - 1)));
         }
         v[e] = x;
@@ -218,10 +231,10 @@ __global__ __launch_bounds__(kBlock) void k_objective_chain(const double *__rest
 
 __global__ __launch_bounds__(kBlock) void k_objective_finish(double *__restrict__ T, Geo g,
                                                              const double *__restrict__ acc,
-                                                             const double *__restrict__ cost) {
+                                                             const double *__restrict__ cost, int64_t orow) {
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= g.ld) return;
-    double *obj = T + g.nloc * g.ld;
+    double *obj = T + orow * g.ld;
     obj[j] = j == 0 ? acc[0] : (j < g.ncols ? acc[j] - cost[j - 1] : 0.0);
 }
 
@@ -232,9 +245,9 @@ int launch_objective_chain(const Launch &L, const Geo &g, const double *cb, cons
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_objective_finish(const Launch &L, const Geo &g, const double *acc, const double *cost) {
+int launch_objective_finish(const Launch &L, const Geo &g, const double *acc, const double *cost, int64_t orow) {
     hipLaunchKernelGGL(k_objective_finish, dim3((unsigned)((g.ld + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       (hipStream_t)L.stream, g.T, g, acc, cost);
+                       (hipStream_t)L.stream, g.T, g, acc, cost, orow);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -264,20 +277,23 @@ __global__ __launch_bounds__(kBlock) void k_price(const double *__restrict__ T, 
     if (MODE == 1 && st->slot[s].status != RUNNING) return;
     const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t nvec = (g.ncols + 1) / 2;
-    PricePart best{0.0, -1};
+    PricePart best{0.0, -1, 0, 0};
     bool live = false;
     if (j2 < nvec) {
-        const d2 d = *(const d2 *)(T + g.nloc * g.ld + 2 * j2);
-        d2 dn = d;
+        const int64_t rM = g.nloc, rR = g.nloc + g.nobj - 1;   // M-part row (Big-M) and real row
+        d2 dM = *(const d2 *)(T + rM * g.ld + 2 * j2);
+        d2 dR = *(const d2 *)(T + rR * g.ld + 2 * j2);
         if (MODE == 1) {
-            const double c = -Cs[g.nloc];
             const d2 p = *(const d2 *)(P + 2 * j2);
-            dn.x = fma(c, p.x, d.x);
-            dn.y = fma(c, p.y, d.y);
+            const double cM = -Cs[rM], cR = -Cs[rR];
+            dM.x = fma(cM, p.x, dM.x);
+            dM.y = fma(cM, p.y, dM.y);
+            dR.x = fma(cR, p.x, dR.x);
+            dR.y = fma(cR, p.y, dR.y);
             live = p.x != 0.0 || p.y != 0.0;
         }
-        price_one<RULE>(best, dn.x, 2 * j2, g);
-        price_one<RULE>(best, dn.y, 2 * j2 + 1, g);
+        price_one<RULE>(best, dM.x, dR.x, 2 * j2, g);
+        price_one<RULE>(best, dM.y, dR.y, 2 * j2 + 1, g);
     }
     if (MODE == 1) count_live(pc, live);
     best = block_reduce_pp<RULE>(best);
@@ -333,7 +349,7 @@ __global__ __launch_bounds__(kBlock) void k_prep(const double *__restrict__ T, G
 
     const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t nvec = (g.ncols + 1) / 2;
-    PricePart pbest{0.0, -1};
+    PricePart pbest{0.0, -1, 0, 0};
     bool live = false;
     if (j2 < nvec) {
         d2 p = d2{0.0, 0.0};
@@ -344,10 +360,12 @@ __global__ __launch_bounds__(kBlock) void k_prep(const double *__restrict__ T, G
         }
         *(d2 *)(P + 2 * j2) = p;
         if (FUSE) {
-            const d2 d = *(const d2 *)(T + g.nloc * g.ld + 2 * j2);
-            const double c = -Cs[g.nloc];
-            price_one<RULE>(pbest, fma(c, p.x, d.x), 2 * j2, g);
-            price_one<RULE>(pbest, fma(c, p.y, d.y), 2 * j2 + 1, g);
+            const int64_t rM = g.nloc, rR = g.nloc + g.nobj - 1;
+            const d2 dM = *(const d2 *)(T + rM * g.ld + 2 * j2);
+            const d2 dR = *(const d2 *)(T + rR * g.ld + 2 * j2);
+            const double cM = -Cs[rM], cR = -Cs[rR];
+            price_one<RULE>(pbest, fma(cM, p.x, dM.x), fma(cR, p.x, dR.x), 2 * j2, g);
+            price_one<RULE>(pbest, fma(cM, p.y, dM.y), fma(cR, p.y, dR.y), 2 * j2 + 1, g);
             live = p.x != 0.0 || p.y != 0.0;
         }
     }
@@ -420,7 +438,7 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
             st->touched += (unsigned long long)tot * (unsigned long long)(g.nloc + g.nobj);
         }
     }
-    PricePart pb{0.0, -1};
+    PricePart pb{0.0, -1, 0, 0};
     if (force_k > 0) {              // forced pivot (lpg_pivot): no pricing
         pb.j = force_k;
         pb.v = -1.0;
@@ -431,7 +449,7 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
         }
         pb = block_reduce_pp<RULE>(pb);
     }
-    const bool optimal = pb.j < 0 || (force_k <= 0 && RULE == RULE_DANTZIG && !(pb.v < -g.eps_opt));
+    const bool optimal = pb.j < 0;   // only eligible columns (d_j < 0, lexicographically) are candidates
     if (optimal) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             dst->status = OPTIMAL;

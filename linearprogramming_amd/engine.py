@@ -53,6 +53,7 @@ class Engine:
         if rc != 0:
             raise LPGError(f"lpg_create_dist rc={rc}: {self.lib.lpg_last_error(None).decode()}")
         self.m, self.ncols, self.world, self.rank = m, ncols, world, rank
+        self.nobj = 2 if flags & L.FLAG_BIG_M else 1
         self._keep = []   # ctypes callbacks kept alive
 
     # -- lifecycle -------------------------------------------------------
@@ -175,6 +176,17 @@ class Engine:
         r = L.Result()
         self._check(self.lib.lpg_solve_two_phase(self._ctx, art_first, cp, max_pivots, rule, ctypes.byref(r)),
                     "lpg_solve_two_phase")
+        return _res(r)
+
+    def set_objective_m(self, cM):
+        c = np.ascontiguousarray(cM, dtype=np.float64)
+        self._check(self.lib.lpg_set_objective_m(self._ctx, c.ctypes.data_as(L.c_double_p)), "lpg_set_objective_m")
+
+    def solve_big_m(self, art_first: int, cost=None, max_pivots: int = 1 << 40, rule: int = L.RULE_DANTZIG):
+        cp = None if cost is None else np.ascontiguousarray(cost, dtype=np.float64).ctypes.data_as(L.c_double_p)
+        r = L.Result()
+        self._check(self.lib.lpg_solve_big_m(self._ctx, art_first, cp, max_pivots, rule, ctypes.byref(r)),
+                    "lpg_solve_big_m")
         return _res(r)
 
     def reserve_log(self, n: int):

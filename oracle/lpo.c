@@ -46,11 +46,13 @@ double lpo_uniform(uint64_t key, uint64_t idx) {
     return (double)(splitmix64(key ^ (idx * 0x9E3779B97F4A7C15ull)) >> 11) * 0x1.0p-53;
 }
 
-lpo_ctx *lpo_create(int64_t m, int64_t ncols, int nthreads) {
-    if (m <= 0 || ncols < 2) return NULL;
+lpo_ctx *lpo_create(int64_t m, int64_t ncols, int nthreads) { return lpo_create2(m, ncols, nthreads, 1); }
+
+lpo_ctx *lpo_create2(int64_t m, int64_t ncols, int nthreads, int nobj) {
+    if (m <= 0 || ncols < 2 || nobj < 1 || nobj > 2) return NULL;
     lpo_ctx *c = (lpo_ctx *)calloc(1, sizeof(lpo_ctx));
     if (!c) return NULL;
-    c->m = m; c->ncols = ncols; c->nobj = 1; c->nact = ncols - 1;
+    c->m = m; c->ncols = ncols; c->nobj = nobj; c->nact = ncols - 1;
     c->ld = (ncols + 7) & ~(int64_t)7;
     c->T = (double *)calloc((size_t)((m + c->nobj) * c->ld), sizeof(double));
     c->P = (double *)calloc((size_t)c->ld, sizeof(double));
@@ -92,9 +94,22 @@ int lpo_set_basis(lpo_ctx *c, const int64_t *basis) {
     return 0;
 }
 
+static int set_objective_row(lpo_ctx *c, const double *cost, int64_t orow);
+
+/* (real) objective row m + nobj - 1 */
 int lpo_set_objective(lpo_ctx *c, const double *cost) {
     if (!c || !cost) return -1;
-    double *obj = c->T + c->m * c->ld;
+    return set_objective_row(c, cost, c->m + c->nobj - 1);
+}
+
+/* Big-M: the M-part row m */
+int lpo_set_objective_m(lpo_ctx *c, const double *cost) {
+    if (!c || !cost || c->nobj != 2) return -1;
+    return set_objective_row(c, cost, c->m);
+}
+
+static int set_objective_row(lpo_ctx *c, const double *cost, int64_t orow) {
+    double *obj = c->T + orow * c->ld;
     /* d_j = sum_i cB_i * T[i][j] - c_j ; sum in row order with fma. */
     for (int64_t j = 0; j < c->ncols; j++) {
         double acc = 0.0;
@@ -161,8 +176,8 @@ int lpo_generate(lpo_ctx *c, int64_t n, uint64_t seed, int kind) {
         row[u] = 1.0;
         c->basis[i] = u;
     }
-    double *obj = c->T + m * ld;
-    memset(obj, 0, (size_t)ld * sizeof(double));
+    for (int64_t q = 0; q < c->nobj; q++) memset(c->T + (m + q) * ld, 0, (size_t)ld * sizeof(double));
+    double *obj = c->T + (m + c->nobj - 1) * ld;   /* (real) objective row; a Big-M M row stays zero */
     for (int64_t j = 0; j < n; j++) obj[1 + j] = -(1.0 + lpo_uniform(kC, (uint64_t)j));
     c->status = LPO_RUNNING;
     c->pivots = 0; c->last_k = c->last_r = -1;
@@ -171,17 +186,31 @@ int lpo_generate(lpo_ctx *c, int64_t n, uint64_t seed, int kind) {
 
 /* ---- pivot rules ---- */
 
-static int64_t price(const lpo_ctx *c, int rule) {
-    const double *d = c->T + c->m * c->ld;
-    if (rule == LPO_RULE_BLAND) {
-        for (int64_t j = 1; j <= c->nact; j++)
-            if (d[j] < -c->eps_opt) return j;
-        return -1;
+/* Eligibility class of column j: -1 not eligible; one objective row: 0 if
+ * d_j < -eps (value d_j); Big-M: 0 if dM_j < -eps (value dM_j), 1 if
+ * |dM_j| <= eps and dR_j < -eps (value dR_j). NaN is never eligible. */
+static int price_class(const lpo_ctx *c, int64_t j, double *v) {
+    const double dR = c->T[(c->m + c->nobj - 1) * c->ld + j];
+    if (c->nobj == 1) {
+        if (!(dR < -c->eps_opt)) return -1;
+        *v = dR;
+        return 0;
     }
-    int64_t best = -1; double bv = 0.0;
-    for (int64_t j = 1; j <= c->nact; j++)   /* NaN entries never win */
-        if (d[j] == d[j] && (best < 0 || d[j] < bv)) { bv = d[j]; best = j; }
-    if (best < 0 || !(bv < -c->eps_opt)) return -1;
+    const double dM = c->T[c->m * c->ld + j];
+    if (dM < -c->eps_opt) { *v = dM; return 0; }
+    if (dM <= c->eps_opt && dR < -c->eps_opt) { *v = dR; return 1; }
+    return -1;
+}
+
+static int64_t price(const lpo_ctx *c, int rule) {
+    int64_t best = -1; int bc = 0; double bv = 0.0;
+    for (int64_t j = 1; j <= c->nact; j++) {
+        double v;
+        const int cls = price_class(c, j, &v);
+        if (cls < 0) continue;
+        if (rule == LPO_RULE_BLAND) return j;
+        if (best < 0 || cls < bc || (cls == bc && v < bv)) { best = j; bc = cls; bv = v; }
+    }
     return best;
 }
 
@@ -268,7 +297,7 @@ int lpo_solve(lpo_ctx *c, int64_t max_pivots, int rule, int nparts, lpo_result *
         out->status = c->status == LPO_RUNNING ? LPO_ITER_LIMIT : c->status;
         out->rule = rule;
         out->pivots = c->pivots;
-        out->objective = c->T[c->m * c->ld];
+        out->objective = c->T[(c->m + c->nobj - 1) * c->ld];
         out->entering = c->last_k;
         out->leaving = c->last_r;
     }
@@ -381,5 +410,31 @@ int lpo_solve_two_phase(lpo_ctx *c, int64_t art_first, const double *cost, int64
     int64_t left = max_pivots - c->pivots;
     lpo_solve(c, left > 0 ? left : 0, rule, 1, out);
     free(own);
+    return 0;
+}
+
+/* Big-M restatement (same algorithm as lpg_solve_big_m): artificial columns
+ * art_first..N cost -M, kept as the M-part objective row. */
+int lpo_solve_big_m(lpo_ctx *c, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
+                    lpo_result *out) {
+    if (!c || c->nobj != 2 || art_first < 2 || art_first >= c->ncols) return -1;
+    const int64_t N = c->ncols - 1;
+    double *cr = (double *)malloc((size_t)N * sizeof(double));
+    double *cm = (double *)calloc((size_t)N, sizeof(double));
+    if (!cr || !cm) { free(cr); free(cm); return -1; }
+    for (int64_t j = 1; j <= N; j++) cr[j - 1] = cost ? cost[j - 1] : -c->T[(c->m + 1) * c->ld + j];
+    for (int64_t j = art_first; j <= N; j++) { cr[j - 1] = 0.0; cm[j - 1] = -1.0; }
+    c->nact = N;
+    lpo_set_objective_m(c, cm);
+    lpo_set_objective(c, cr);
+    free(cr); free(cm);
+    lpo_result r;
+    lpo_solve(c, max_pivots, rule, 1, &r);
+    if (r.status == LPO_OPTIMAL) {
+        double bsum = 0;
+        for (int64_t i = 0; i < c->m; i++) bsum += fabs(c->T[i * c->ld]);
+        if (c->T[c->m * c->ld] < -1e-9 * (bsum > 1.0 ? bsum : 1.0)) r.status = LPO_INFEASIBLE;
+    }
+    if (out) *out = r;
     return 0;
 }

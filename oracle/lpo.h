@@ -59,12 +59,15 @@ typedef struct {
 
 /* m constraint rows, ncols = N+1 columns (b + N variables). */
 lpo_ctx *lpo_create(int64_t m, int64_t ncols, int nthreads);
+/* nobj = 2: Big-M layout (row m = M part, row m+1 = real part). */
+lpo_ctx *lpo_create2(int64_t m, int64_t ncols, int nthreads, int nobj);
 void     lpo_destroy(lpo_ctx *ctx);
 int      lpo_load_rows(lpo_ctx *ctx, int64_t row0, int64_t nrows, const double *rows, int64_t ld);
 int      lpo_set_basis(lpo_ctx *ctx, const int64_t *basis);
 /* Objective row from costs c[0..N-1] (max c.x) and the current basis:
  * d_j = sum_i c_B(i) T[i][j] - c_j, z = sum_i c_B(i) b_i (row order fixed). */
 int      lpo_set_objective(lpo_ctx *ctx, const double *c);
+int      lpo_set_objective_m(lpo_ctx *ctx, const double *c);
 int      lpo_generate(lpo_ctx *ctx, int64_t n_struct, uint64_t seed, int kind);
 int64_t  lpo_unit_column(int64_t m, int64_t n, int64_t i, int kind);
 int      lpo_set_tolerances(lpo_ctx *ctx, double eps_piv, double eps_opt);
@@ -88,6 +91,11 @@ int      lpo_pivot(lpo_ctx *ctx, int64_t k, int64_t r);
  * costs are -1 x the objective row as loaded, i.e. a slack-form -c row). */
 int      lpo_solve_two_phase(lpo_ctx *ctx, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
                              lpo_result *out);
+
+/* Big-M method, same algorithm as lpg_solve_big_m (cost NULL: -1 x the
+ * real objective row as loaded). */
+int      lpo_solve_big_m(lpo_ctx *ctx, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
+                         lpo_result *out);
 
 /* Row-block primitives for the multi-rank protocol model (tests only). */
 int64_t  lpo_price_col(const lpo_ctx *ctx, int rule);

@@ -50,6 +50,10 @@ def load():
         lib = ctypes.CDLL(LIB_PATH)
         sig = {
             "lpo_create": (ctypes.c_void_p, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int]),
+            "lpo_create2": (ctypes.c_void_p, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int]),
+            "lpo_set_objective_m": (ctypes.c_int, [ctypes.c_void_p, _dp]),
+            "lpo_solve_big_m": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _dp, ctypes.c_int64, ctypes.c_int,
+                                               ctypes.POINTER(_Result)]),
             "lpo_destroy": (None, [ctypes.c_void_p]),
             "lpo_load_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, _dp, ctypes.c_int64]),
             "lpo_set_basis": (ctypes.c_int, [ctypes.c_void_p, _ip]),
@@ -81,10 +85,10 @@ def load():
 
 
 class Oracle:
-    def __init__(self, m: int, ncols: int, nthreads: int = 1):
+    def __init__(self, m: int, ncols: int, nthreads: int = 1, nobj: int = 1):
         self.lib = load()
-        self.m, self.ncols = m, ncols
-        self.ctx = self.lib.lpo_create(m, ncols, nthreads)
+        self.m, self.ncols, self.nobj = m, ncols, nobj
+        self.ctx = self.lib.lpo_create2(m, ncols, nthreads, nobj)
         if not self.ctx:
             raise RuntimeError("lpo_create failed")
 
@@ -113,6 +117,16 @@ class Oracle:
     def set_objective(self, c):
         c = np.ascontiguousarray(c, dtype=np.float64)
         self._ok(self.lib.lpo_set_objective(self.ctx, c.ctypes.data_as(_dp)), "set_objective")
+
+    def set_objective_m(self, c):
+        c = np.ascontiguousarray(c, dtype=np.float64)
+        self._ok(self.lib.lpo_set_objective_m(self.ctx, c.ctypes.data_as(_dp)), "set_objective_m")
+
+    def solve_big_m(self, art_first: int, cost=None, max_pivots: int = 1 << 40, rule: int = RULE_DANTZIG):
+        cp = None if cost is None else np.ascontiguousarray(cost, dtype=np.float64).ctypes.data_as(_dp)
+        r = _Result()
+        self._ok(self.lib.lpo_solve_big_m(self.ctx, art_first, cp, max_pivots, rule, ctypes.byref(r)), "solve_big_m")
+        return OracleResult(r.status, r.pivots, r.objective, r.entering, r.leaving)
 
     def set_tolerances(self, eps_piv=1e-9, eps_opt=1e-9):
         self._ok(self.lib.lpo_set_tolerances(self.ctx, eps_piv, eps_opt), "set_tolerances")
@@ -158,7 +172,7 @@ class Oracle:
 
     def get_rows(self, row0=0, nrows=None) -> np.ndarray:
         if nrows is None:
-            nrows = self.m + 1 - row0
+            nrows = self.m + self.nobj - row0
         out = np.zeros((nrows, self.ncols))
         self._ok(self.lib.lpo_get_rows(self.ctx, row0, nrows, out.ctypes.data_as(_dp), self.ncols), "get_rows")
         return out
