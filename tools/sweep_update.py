@@ -22,8 +22,10 @@ ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--steps", type=int, default=30)
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--variants", default="")
+ap.add_argument("--m", type=int, default=0, help="custom shape (overrides --config)")
+ap.add_argument("--n", type=int, default=0)
 a = ap.parse_args()
-m, n = CONFIGS[a.config]
+m, n = (a.m, a.n) if a.m else CONFIGS[a.config]
 lib = lpg.load()
 nvar = 25
 variants = [int(v) for v in a.variants.split(",")] if a.variants else list(range(nvar))
@@ -53,7 +55,7 @@ for rnd in range(a.rounds):
 summary = {v: {"best_ms": min(x["update_ms"] for x in res[v]), "best_GBps": max(x["GBps"] for x in res[v]),
                "runs": res[v]} for v in variants}
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-with open(os.path.join(ROOT, "gpurun_out", f"sweep_config{a.config}.json"), "w") as f:
+with open(os.path.join(ROOT, "gpurun_out", f"sweep_{m}x{n}.json"), "w") as f:
     json.dump(summary, f, indent=1)
 for v in sorted(variants, key=lambda v: summary[v]["best_ms"]):
     print(f"variant {v:2d}: best {summary[v]['best_ms']:.4f} ms {summary[v]['best_GBps']:.1f} GB/s")
