@@ -716,13 +716,14 @@ int update_variants() { return kNumUpdateCfgs; }
 // Default (variant < 0): large tableaus use the persistent grid with a
 // dynamic dequeue, non-temporal streaming and pipelined rows (variant 21:
 // steady at the read-modify-write ceiling when skipped columns make the work
-// per tile uneven); small ones (fewer than 8192 work items, e.g. config 2)
+// per tile uneven; measured best from 2048 to 16385 rows); small ones (fewer
+// than 2048 work items, e.g. config 2, MALL-resident)
 // use one block per item (variant 0), where the dequeue atomics would cost
 // more than they balance.
 int update_auto_variant(const Geo &g) {
     const int64_t nvec = (g.ncols + 1) / 2;
     const int64_t items = ((nvec + kBlock - 1) / kBlock) * ((g.nloc + g.nobj + 63) / 64);
-    return items >= 8192 ? 21 : 0;
+    return items >= 2048 ? 21 : 0;
 }
 
 int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
