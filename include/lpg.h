@@ -67,6 +67,8 @@ extern "C" {
 /* ---- synthetic generators (device-side) ---- */
 #define LPG_GEN_DENSE      0  /* A_ij = u, b_i = n/8 (1+u), c_j = 1+u, <= rows, slack basis */
 #define LPG_GEN_DEGENERATE 1  /* lower-triangular KM-style rows (a_ii = 1, a_ij = u/(i+1)), b_i = 0 on even rows */
+#define LPG_GEN_DUAL       3  /* dual-simplex LP: min c.x, A x >= b (A = u, b = n/8 (1+u), c = 1+u) as
+                                 rows [-b | -A | I], objective row [0 | c | 0] */
 #define LPG_GEN_ARTIFICIAL 2  /* config 5: KM-style; even rows `<= 0` (a_ij = -u/(i+1)), odd rows equalities whose
                                  unit columns are artificials at columns 1+n+ceil(m/2) .. N */
 
@@ -195,6 +197,15 @@ int  lpg_solve_two_phase(lpg_ctx *ctx, int64_t art_first, const double *cost, in
  * row as loaded. */
 int  lpg_solve_big_m(lpg_ctx *ctx, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
                      lpg_result *out);
+
+/* Dual simplex (reference: router option 2, router.c:32-34, a no-op; the
+ * tableau LPStandardize(model, 1) builds by flipping >= rows, simplex.c:178-179).
+ * Needs a dual-feasible basis (every d_j >= -eps_opt, else LPG_ERR_STATE).
+ * Leaving row: most negative b_i < -eps_opt (ties: smallest row); entering
+ * column: min d_j / (-a_rj) over a_rj < -eps_piv (ties: smallest j); none ->
+ * LPG_INFEASIBLE; no negative b -> LPG_OPTIMAL. Same update kernel and
+ * arithmetic as the primal loop. Single rank. */
+int  lpg_solve_dual(lpg_ctx *ctx, int64_t max_pivots, lpg_result *out);
 
 /* ---- readout ---- */
 int  lpg_get_rows(lpg_ctx *ctx, int64_t row0, int64_t nrows, double *out, int64_t ld);

@@ -18,7 +18,7 @@ OK, ERR_ARG, ERR_DEVICE, ERR_OOM, ERR_STATE, ERR_COMM = 0, -1, -2, -3, -4, -5
 RUNNING, OPTIMAL, UNBOUNDED, INFEASIBLE, ITER_LIMIT, NUMERIC = 0, 1, 2, 3, 4, 5
 STATUS_NAMES = {0: "RUNNING", 1: "OPTIMAL", 2: "UNBOUNDED", 3: "INFEASIBLE", 4: "ITER_LIMIT", 5: "NUMERIC"}
 RULE_DANTZIG, RULE_BLAND = 0, 1
-GEN_DENSE, GEN_DEGENERATE, GEN_ARTIFICIAL = 0, 1, 2
+GEN_DENSE, GEN_DEGENERATE, GEN_ARTIFICIAL, GEN_DUAL = 0, 1, 2, 3
 FLAG_NO_LOG = 0x1
 FLAG_NO_SKIP = 0x2
 FLAG_BIG_M = 0x4
@@ -81,6 +81,7 @@ PROTOTYPES = [
                                            ctypes.POINTER(Result)]),
     ("lpg_solve_big_m", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, c_double_p, ctypes.c_int64, ctypes.c_int,
                                        ctypes.POINTER(Result)]),
+    ("lpg_solve_dual", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(Result)]),
     ("lpg_get_rows", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, c_double_p, ctypes.c_int64]),
     ("lpg_get_basis", ctypes.c_int, [ctypes.c_void_p, c_int64_p]),
     ("lpg_get_column0", ctypes.c_int, [ctypes.c_void_p, c_double_p]),

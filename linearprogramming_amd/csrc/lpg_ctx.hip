@@ -641,7 +641,7 @@ int lpg_set_active_columns(lpg_ctx *c, int64_t nact) {
 }
 
 int lpg_generate(lpg_ctx *c, int64_t n, uint64_t seed, int kind) {
-    if (!c || n < 1 || c->ncols != n + c->m + 1 || kind < LPG_GEN_DENSE || kind > LPG_GEN_ARTIFICIAL)
+    if (!c || n < 1 || c->ncols != n + c->m + 1 || kind < LPG_GEN_DENSE || kind > LPG_GEN_DUAL)
         return fail(c, LPG_ERR_ARG, "lpg_generate: need ncols == n + m + 1 and a known kind");
     int rc;
     if ((rc = use_device(c))) return rc;
@@ -813,6 +813,60 @@ int lpg_solve_big_m(lpg_ctx *c, int64_t art_first, const double *cost, int64_t m
         for (double v : xb) bsum += fabs(v);
         if (zM < -1e-9 * std::max(1.0, bsum)) r.status = LPG_INFEASIBLE;
     }
+    if (out) *out = r;
+    return 0;
+}
+
+int lpg_solve_dual(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
+    if (!c || max_pivots < 0) return fail(c, LPG_ERR_ARG, "lpg_solve_dual: bad arguments");
+    if (c->world != 1 || has_comm(c)) return fail(c, LPG_ERR_STATE, "lpg_solve_dual: single rank only");
+    int rc;
+    if ((rc = use_device(c))) return rc;
+    // the dual simplex starts from a dual-feasible basis: every d_j >= -eps
+    std::vector<double> obj(c->ncols);
+    if ((rc = lpg_get_rows(c, c->m + c->nobj - 1, 1, obj.data(), c->ncols))) return rc;
+    for (int64_t j = 1; j <= c->nact; j++)
+        if (obj[j] < -c->eps_opt)
+            return fail(c, LPG_ERR_STATE, "lpg_solve_dual: basis not dual feasible (d_%lld = %g)", (long long)j, obj[j]);
+    if ((rc = ensure_log(c, c->enq + max_pivots))) return rc;
+    const Geo g = geo(c);
+    const Launch L = lau(c);
+    HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
+    if (launch_dual_rows(L, g, c->part, c->nsel)) return fail(c, LPG_ERR_DEVICE, "dual rows launch failed");
+    c->par = 0;
+    c->booted = false;   // the primal loop must re-price after a dual solve
+    int64_t done = 0, batch = 8;
+    lpg_result r;
+    while (done < max_pivots) {
+        const int64_t n = std::min(batch, max_pivots - done);
+        for (int64_t q = 0; q < n; q++) {
+            const int s = c->par;
+            if (launch_dual_pivot(L, g, c->st, s, c->part, c->nsel, c->pp, c->pc, c->npp, c->skip, c->P, c->C[s]))
+                return fail(c, LPG_ERR_DEVICE, "dual pivot launch failed");
+            if (launch_update(L, g, c->st, s, c->P, c->C[s], c->basis, c->logk, c->logr, c->update_variant, c->skip))
+                return fail(c, LPG_ERR_DEVICE, "update launch failed");
+            c->par = s ^ 1;
+            c->enq++;
+        }
+        done += n;
+        DevState h;
+        HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (h.slot[c->par].status != LPG_RUNNING) break;
+        batch = std::min<int64_t>(batch * 2, 256);
+    }
+    DevState h;
+    double z = 0;
+    HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&z, c->T + (c->nloc + c->nobj - 1) * c->ld, sizeof z, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int32_t st = h.slot[c->par].status;
+    r.status = st == LPG_RUNNING ? LPG_ITER_LIMIT : st;
+    r.rule = LPG_RULE_DANTZIG;
+    r.pivots = h.pivots;
+    r.objective = z;
+    r.entering = h.pivots ? h.last_k : -1;
+    r.leaving = h.pivots ? h.last_r : -1;
     if (out) *out = r;
     return 0;
 }

@@ -89,6 +89,10 @@ int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState 
 int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
                   int64_t *basis, int64_t *logk, int64_t *logr, int variant, int skip);
 
+int launch_dual_rows(const Launch &L, const Geo &g, Cand *part, int nsel);
+int launch_dual_pivot(const Launch &L, const Geo &g, DevState *st, int s, Cand *part, int nsel, PricePart *pp,
+                      int *pc, int npp, int skip, double *P, double *Cs);
+
 int price_blocks(const Geo &g);      // number of pricing partials (= prep / price grid)
 int update_variants();               // entries of the update-kernel variant table
 int update_auto_variant(const Geo &g);   // default variant for this geometry

@@ -173,12 +173,14 @@ __global__ __launch_bounds__(kBlock) void k_generate(double *__restrict__ T, Geo
         if (i < g.nloc) {
             const int64_t gi = g.row0 + i;
             if (j == 0) {
-                if (kind == 0 || (gi & 1))
+                if (kind == 0 || kind == 3 || (gi & 1))
                     x = bscale * (1.0 + uniform01(kB, (uint64_t)gi));
+                if (kind == 3) x = -x;
             } else if (j <= n) {
                 const int64_t jj = j - 1;
-                if (kind == 0) {
+                if (kind == 0 || kind == 3) {
                     x = uniform01(kA, (uint64_t)(gi * n + jj));
+                    if (kind == 3) x = -x;
                 } else {
                     const double sgn = (kind == 2 && !(gi & 1)) ? -1.0 : 1.0;
                     if (jj < gi) x = sgn * (uniform01(kA, (uint64_t)(gi * n + jj)) / (double)(gi + 1));
@@ -188,7 +190,10 @@ __global__ __launch_bounds__(kBlock) void k_generate(double *__restrict__ T, Geo
                 x = 1.0;
             }
         } else if (i == g.nloc + g.nobj - 1) {   // (real) objective row; a Big-M M row stays zero
-            if (j >= 1 && j <= n) x = -(1.0 + uniform01(kC, (uint64_t)(j - 1)));
+            if (j >= 1 && j <= n) {
+                x = 1.0 + uniform01(kC, (uint64_t)(j - 1));
+                if (kind != 3) x = -x;            // kind 3: max -c.x, d_j = +c_j (dual feasible)
+            }
         }
         v[e] = x;
     }
@@ -519,6 +524,183 @@ int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState 
         if (first) LPG_SEL(RULE_DANTZIG, true); else LPG_SEL(RULE_DANTZIG, false);
     }
 #undef LPG_SEL
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------
+// Dual simplex (reference: router option 2, router.c:32-34, a no-op; the
+// tableau LPStandardize(model, 1) builds, simplex.c:178-179). Same update
+// kernel; the pricing roles swap. Pivot t:
+//   k_dual_price : leaving row r_t = argmin b_i over b_i < -eps (ties: smallest
+//                  row) from the row candidates of the previous step; ratio
+//                  test over row r_t: argmin d_j / (-a_rj) over a_rj < -eps_piv
+//                  (ties: smallest j) -> per-block partials; live-slice counts
+//   k_dual_prep  : entering column k_t; P = T[r]/T[r][k]; C = column k; the
+//                  next step's row candidates from b' = fma(-C, P[0], b)
+//   k_update     : as in the primal
+// Single rank.
+// ------------------------------------------------------------------------
+
+// Row candidate: (theta = b_i, key = row) through the Cand min-reduction.
+__device__ __forceinline__ void dual_row_cand(Cand &best, double b, int64_t grow, const Geo &g) {
+    if (!(b < -g.eps_opt)) return;
+    Cand c;
+    c.theta = b;
+    c.piv = 0.0;
+    c.key = grow;
+    c.row = grow;
+    if (cand_better(c, best)) best = c;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dual_rows(const double *__restrict__ T, Geo g, Cand *__restrict__ part) {
+    Cand best{0.0, 0.0, 0, -1};
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < g.nloc; i += (int64_t)gridDim.x * kBlock)
+        dual_row_cand(best, T[i * g.ld], g.row0 + i, g);
+    best = block_reduce_cand(best);
+    if (threadIdx.x == 0) part[blockIdx.x] = best;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dual_price(const double *__restrict__ T, Geo g, DevState *st, int s,
+                                                       const Cand *__restrict__ part, int npart,
+                                                       PricePart *__restrict__ pp, int *__restrict__ pc) {
+    if (st->slot[s].status != RUNNING) return;
+    Cand best{0.0, 0.0, 0, -1};
+    for (int q = threadIdx.x; q < npart; q += kBlock) {
+        const Cand c = part[q];
+        if (cand_better(c, best)) best = c;
+    }
+    best = block_reduce_cand(best);
+    if (best.row < 0) {                      // primal feasible: optimal
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->slot[s].status = OPTIMAL;
+            st->slot[s].r = -1;
+        }
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->slot[s].r = best.row;
+        st->work[s] = 0;
+    }
+    const int64_t rl = best.row - g.row0;
+    const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t nvec = (g.ncols + 1) / 2;
+    PricePart pb{0.0, -1, 0, 0};
+    bool live = false;
+    if (j2 < nvec) {
+        const d2 a = *(const d2 *)(T + rl * g.ld + 2 * j2);
+        const d2 d = *(const d2 *)(T + (g.nloc + g.nobj - 1) * g.ld + 2 * j2);
+        live = a.x != 0.0 || a.y != 0.0;     // P = row / pivot is non-zero exactly here
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const int64_t j = 2 * j2 + e;
+            const double aj = e ? a.y : a.x, dj = e ? d.y : d.x;
+            if (j < 1 || j > g.nact || !(aj < -g.eps_piv)) continue;
+            PricePart c;
+            c.v = dj > 0.0 ? dj / -aj : 0.0;
+            c.j = j;
+            c.cls = 0;
+            c.pad = 0;
+            if (pp_better<RULE_DANTZIG>(c, pb)) pb = c;
+        }
+    }
+    count_live(pc, live);
+    pb = block_reduce_pp<RULE_DANTZIG>(pb);
+    if (threadIdx.x == 0) pp[blockIdx.x] = pb;
+}
+
+// Blocks [0, npp): P; blocks [npp, npp + nsel): column snapshot C and the next
+// step's row candidates.
+__global__ __launch_bounds__(kBlock) void k_dual_prep(const double *__restrict__ T, Geo g, DevState *st, int s,
+                                                      int s1, const PricePart *__restrict__ pp, int npp,
+                                                      const int *__restrict__ pc, int skip, double *__restrict__ P,
+                                                      double *__restrict__ Cs, Cand *__restrict__ part) {
+    const int32_t stt = st->slot[s].status;
+    if (stt != RUNNING) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->slot[s1].status = stt;
+            st->slot[s1].k = -1;
+            st->slot[s1].r = -1;
+        }
+        return;
+    }
+    PricePart pb{0.0, -1, 0, 0};
+    for (int q = threadIdx.x; q < npp; q += kBlock) {
+        const PricePart c = pp[q];
+        if (pp_better<RULE_DANTZIG>(c, pb)) pb = c;
+    }
+    pb = block_reduce_pp<RULE_DANTZIG>(pb);
+    if (pb.j < 0) {                          // no a_rj < 0: the LP is primal infeasible
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->slot[s].status = INFEASIBLE;
+            st->slot[s1].status = INFEASIBLE;
+            st->slot[s1].k = -1;
+            st->slot[s1].r = -1;
+        }
+        return;
+    }
+    const int64_t k = pb.j;
+    const int64_t r = st->slot[s].r;
+    const int64_t rl = r - g.row0;
+    const double piv = T[rl * g.ld + k];
+    const double p0 = T[rl * g.ld] / piv;     // == P[0]
+    if (blockIdx.x == 0) {
+        int64_t live = 0;
+        const int64_t nvec = (g.ncols + 1) / 2;
+        if (skip)
+            for (int q = threadIdx.x; q < npp; q += kBlock) live += pc[q];
+        else if (threadIdx.x == 0)
+            live = nvec;
+#pragma unroll
+        for (int mask = 32; mask > 0; mask >>= 1) live += __shfl_xor((long long)live, mask, 64);
+        __shared__ int64_t wsum[kBlock / 64];
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = live;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t tot = 0;
+            for (int w = 0; w < kBlock / 64; w++) tot += wsum[w];
+            st->touched += (unsigned long long)tot * (unsigned long long)(g.nloc + g.nobj);
+            st->slot[s].k = k;
+            st->slot[s1].status = RUNNING;
+            st->slot[s1].k = -1;
+        }
+    }
+    if ((int)blockIdx.x < npp) {
+        const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+        if (j2 < (g.ncols + 1) / 2) {
+            const d2 t = *(const d2 *)(T + rl * g.ld + 2 * j2);
+            d2 p;
+            p.x = t.x / piv;
+            p.y = t.y / piv;
+            *(d2 *)(P + 2 * j2) = p;
+        }
+        return;
+    }
+    const int64_t nrows = g.nloc + g.nobj;
+    const int64_t nb = (int64_t)gridDim.x - npp;
+    Cand best{0.0, 0.0, 0, -1};
+    for (int64_t i = ((int64_t)blockIdx.x - npp) * kBlock + threadIdx.x; i < nrows; i += nb * kBlock) {
+        const double c = T[i * g.ld + k];
+        Cs[i] = c;
+        if (i < g.nloc) {
+            const double b = i == rl ? p0 : fma(-c, p0, T[i * g.ld]);
+            dual_row_cand(best, b, g.row0 + i, g);
+        }
+    }
+    best = block_reduce_cand(best);
+    if (threadIdx.x == 0) part[blockIdx.x - npp] = best;
+}
+
+int launch_dual_rows(const Launch &L, const Geo &g, Cand *part, int nsel) {
+    hipLaunchKernelGGL(k_dual_rows, dim3(nsel), dim3(kBlock), 0, (hipStream_t)L.stream, g.T, g, part);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_dual_pivot(const Launch &L, const Geo &g, DevState *st, int s, Cand *part, int nsel, PricePart *pp,
+                      int *pc, int npp, int skip, double *P, double *Cs) {
+    hipStream_t stream = (hipStream_t)L.stream;
+    hipLaunchKernelGGL(k_dual_price, dim3(npp), dim3(kBlock), 0, stream, g.T, g, st, s, part, nsel, pp, pc);
+    hipLaunchKernelGGL(k_dual_prep, dim3(npp + nsel), dim3(kBlock), 0, stream, g.T, g, st, s, s ^ 1, pp, npp, pc,
+                       skip, P, Cs, part);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -189,6 +189,11 @@ class Engine:
                     "lpg_solve_big_m")
         return _res(r)
 
+    def solve_dual(self, max_pivots: int = 1 << 40) -> SolveResult:
+        r = L.Result()
+        self._check(self.lib.lpg_solve_dual(self._ctx, max_pivots, ctypes.byref(r)), "lpg_solve_dual")
+        return _res(r)
+
     def reserve_log(self, n: int):
         self._check(self.lib.lpg_reserve_log(self._ctx, n), "lpg_reserve_log")
 

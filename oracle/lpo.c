@@ -151,7 +151,7 @@ int64_t lpo_unit_column(int64_t m, int64_t n, int64_t i, int kind) {
  * `<= 0` row) and odd rows are equalities whose unit columns are artificial
  * (columns art_first..N); the objective row still holds -c. */
 int lpo_generate(lpo_ctx *c, int64_t n, uint64_t seed, int kind) {
-    if (!c || n < 1 || c->ncols != n + c->m + 1 || kind < 0 || kind > LPO_GEN_ARTIFICIAL) return -1;
+    if (!c || n < 1 || c->ncols != n + c->m + 1 || kind < 0 || kind > LPO_GEN_DUAL) return -1;
     const int64_t m = c->m, ld = c->ld;
     const uint64_t kA = lpo_subkey(seed, 1), kB = lpo_subkey(seed, 2), kC = lpo_subkey(seed, 3);
     const double bscale = (double)n / 8.0;
@@ -159,9 +159,10 @@ int lpo_generate(lpo_ctx *c, int64_t n, uint64_t seed, int kind) {
     for (int64_t i = 0; i < m; i++) {
         double *row = c->T + i * ld;
         memset(row, 0, (size_t)ld * sizeof(double));
-        if (kind == LPO_GEN_DENSE) {
-            row[0] = bscale * (1.0 + lpo_uniform(kB, (uint64_t)i));
-            for (int64_t j = 0; j < n; j++) row[1 + j] = lpo_uniform(kA, (uint64_t)(i * n + j));
+        if (kind == LPO_GEN_DENSE || kind == LPO_GEN_DUAL) {
+            const double sg = kind == LPO_GEN_DUAL ? -1.0 : 1.0;   /* dual: rows [-b | -A | I] */
+            row[0] = sg * (bscale * (1.0 + lpo_uniform(kB, (uint64_t)i)));
+            for (int64_t j = 0; j < n; j++) row[1 + j] = sg * lpo_uniform(kA, (uint64_t)(i * n + j));
         } else {
             row[0] = (i & 1) ? bscale * (1.0 + lpo_uniform(kB, (uint64_t)i)) : 0.0;
             const double sgn = (kind == LPO_GEN_ARTIFICIAL && !(i & 1)) ? -1.0 : 1.0;
@@ -178,7 +179,10 @@ int lpo_generate(lpo_ctx *c, int64_t n, uint64_t seed, int kind) {
     }
     for (int64_t q = 0; q < c->nobj; q++) memset(c->T + (m + q) * ld, 0, (size_t)ld * sizeof(double));
     double *obj = c->T + (m + c->nobj - 1) * ld;   /* (real) objective row; a Big-M M row stays zero */
-    for (int64_t j = 0; j < n; j++) obj[1 + j] = -(1.0 + lpo_uniform(kC, (uint64_t)j));
+    for (int64_t j = 0; j < n; j++) {
+        const double cj = 1.0 + lpo_uniform(kC, (uint64_t)j);
+        obj[1 + j] = kind == LPO_GEN_DUAL ? cj : -cj;   /* dual: max -c.x, d_j = +c_j */
+    }
     c->status = LPO_RUNNING;
     c->pivots = 0; c->last_k = c->last_r = -1;
     return 0;
@@ -436,5 +440,51 @@ int lpo_solve_big_m(lpo_ctx *c, int64_t art_first, const double *cost, int64_t m
         if (c->T[c->m * c->ld] < -1e-9 * (bsum > 1.0 ? bsum : 1.0)) r.status = LPO_INFEASIBLE;
     }
     if (out) *out = r;
+    return 0;
+}
+
+/* Dual simplex restatement (same rules as lpg_solve_dual): leaving row =
+ * most negative b_i < -eps_opt (ties: smallest row); entering column =
+ * min d_j / (-a_rj) over a_rj < -eps_piv (ties: smallest j). */
+int lpo_solve_dual(lpo_ctx *c, int64_t max_pivots, lpo_result *out) {
+    if (!c || max_pivots < 0) return -1;
+    const double *d = c->T + (c->m + c->nobj - 1) * c->ld;
+    for (int64_t j = 1; j <= c->nact; j++)
+        if (d[j] < -c->eps_opt) return -2;            /* not dual feasible */
+    int status = LPO_RUNNING;
+    int64_t done = 0;
+    while (done < max_pivots) {
+        int64_t r = -1; double br = 0.0;
+        for (int64_t i = 0; i < c->m; i++) {
+            const double b = c->T[i * c->ld];
+            if (b < -c->eps_opt && (r < 0 || b < br)) { r = i; br = b; }
+        }
+        if (r < 0) { status = LPO_OPTIMAL; break; }
+        int64_t k = -1; double best = 0.0;
+        const double *row = c->T + r * c->ld;
+        d = c->T + (c->m + c->nobj - 1) * c->ld;
+        for (int64_t j = 1; j <= c->nact; j++) {
+            const double a = row[j];
+            if (!(a < -c->eps_piv)) continue;
+            const double v = d[j] > 0.0 ? d[j] / -a : 0.0;
+            if (k < 0 || v < best) { k = j; best = v; }
+        }
+        if (k < 0) { status = LPO_INFEASIBLE; break; }
+        if (lpo_pivot(c, k, r) != 0) return -1;
+        done++;
+    }
+    if (status == LPO_RUNNING) {                        /* peek, like the device's last step */
+        int any = 0;
+        for (int64_t i = 0; i < c->m; i++) any |= c->T[i * c->ld] < -c->eps_opt;
+        status = any ? LPO_ITER_LIMIT : LPO_OPTIMAL;
+    }
+    if (out) {
+        out->status = status;
+        out->rule = LPO_RULE_DANTZIG;
+        out->pivots = c->pivots;
+        out->objective = c->T[(c->m + c->nobj - 1) * c->ld];
+        out->entering = c->last_k;
+        out->leaving = c->last_r;
+    }
     return 0;
 }

@@ -44,7 +44,7 @@ extern "C" {
 enum { LPO_RUNNING = 0, LPO_OPTIMAL = 1, LPO_UNBOUNDED = 2, LPO_INFEASIBLE = 3,
        LPO_ITER_LIMIT = 4, LPO_NUMERIC = 5 };
 enum { LPO_RULE_DANTZIG = 0, LPO_RULE_BLAND = 1 };
-enum { LPO_GEN_DENSE = 0, LPO_GEN_DEGENERATE = 1, LPO_GEN_ARTIFICIAL = 2 };
+enum { LPO_GEN_DENSE = 0, LPO_GEN_DEGENERATE = 1, LPO_GEN_ARTIFICIAL = 2, LPO_GEN_DUAL = 3 };
 
 typedef struct lpo_ctx lpo_ctx;
 
@@ -96,6 +96,10 @@ int      lpo_solve_two_phase(lpo_ctx *ctx, int64_t art_first, const double *cost
  * real objective row as loaded). */
 int      lpo_solve_big_m(lpo_ctx *ctx, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
                          lpo_result *out);
+
+/* Dual simplex, same rules as lpg_solve_dual; -2 if the basis is not dual
+ * feasible. */
+int      lpo_solve_dual(lpo_ctx *ctx, int64_t max_pivots, lpo_result *out);
 
 /* Row-block primitives for the multi-rank protocol model (tests only). */
 int64_t  lpo_price_col(const lpo_ctx *ctx, int rule);

@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblpo.so")
 
 RULE_DANTZIG, RULE_BLAND = 0, 1
-GEN_DENSE, GEN_DEGENERATE, GEN_ARTIFICIAL = 0, 1, 2
+GEN_DENSE, GEN_DEGENERATE, GEN_ARTIFICIAL, GEN_DUAL = 0, 1, 2, 3
 STATUS_NAMES = {0: "RUNNING", 1: "OPTIMAL", 2: "UNBOUNDED", 3: "INFEASIBLE", 4: "ITER_LIMIT", 5: "NUMERIC"}
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -74,6 +74,7 @@ def load():
             "lpo_apply": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, _dp]),
             "lpo_solve_two_phase": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _dp, ctypes.c_int64, ctypes.c_int,
                                                    ctypes.POINTER(_Result)]),
+            "lpo_solve_dual": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(_Result)]),
             "lpo_uniform": (ctypes.c_double, [ctypes.c_uint64, ctypes.c_uint64]),
             "lpo_subkey": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
         }
@@ -147,6 +148,11 @@ class Oracle:
         r = _Result()
         self._ok(self.lib.lpo_solve_two_phase(self.ctx, art_first, cp, max_pivots, rule, ctypes.byref(r)),
                  "solve_two_phase")
+        return OracleResult(r.status, r.pivots, r.objective, r.entering, r.leaving)
+
+    def solve_dual(self, max_pivots: int = 1 << 40) -> OracleResult:
+        r = _Result()
+        self._ok(self.lib.lpo_solve_dual(self.ctx, max_pivots, ctypes.byref(r)), "solve_dual")
         return OracleResult(r.status, r.pivots, r.objective, r.entering, r.leaving)
 
     def pivot(self, k: int, r: int):

@@ -65,10 +65,11 @@ def synthetic(m: int, n: int, seed: int, kind: int):
     T = []
     for i in range(m):
         row = [0.0] * (n + m + 1)
-        if kind == 0:
-            row[0] = bscale * (1.0 + uniform(kB, i))
+        if kind in (0, 3):
+            sg = -1.0 if kind == 3 else 1.0          # kind 3 (dual): rows [-b | -A | I]
+            row[0] = sg * (bscale * (1.0 + uniform(kB, i)))
             for j in range(n):
-                row[1 + j] = uniform(kA, i * n + j)
+                row[1 + j] = sg * uniform(kA, i * n + j)
         else:
             row[0] = bscale * (1.0 + uniform(kB, i)) if i & 1 else 0.0
             sgn = -1.0 if (kind == 2 and not i & 1) else 1.0
@@ -78,7 +79,8 @@ def synthetic(m: int, n: int, seed: int, kind: int):
         T.append(row)
     obj = [0.0] * (n + m + 1)
     for j in range(n):
-        obj[1 + j] = -(1.0 + uniform(kC, j))
+        cj = 1.0 + uniform(kC, j)
+        obj[1 + j] = cj if kind == 3 else -cj
     T.append(obj)
     basis = [unit_column(m, n, i, kind) for i in range(m)]
     return T, basis
