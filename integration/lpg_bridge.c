@@ -11,6 +11,9 @@
  * a maintainer adopting the engine would instead call LPGSolveSMatrix() from
  * simplex.c:40 directly.
  *
+ * Artificials: rows without a unit basic column are given artificial columns
+ * and solved by two-phase (default) or Big-M (LPG_ARTIFICIAL=bigm).
+ *
  * Conversion (SURVEY.md §8(b) "build-side caller"): every cell through the
  * reference's own Decimalize (Source/basicFuncs.c:298-313), the basis from
  * SimplexMatrix.basicVars (which alias varNames, matrix.c:76-77), costs from
@@ -35,44 +38,72 @@ static double value_of(const char *name, char **varNames, const double *x, size_
 }
 
 /* Solve one CreateSMatrix tableau on the device and print the optimum in the
- * reference's style. Returns 1 (valid) on success, 0 otherwise. */
+ * reference's style. Rows without a true unit basic column (CreateSMatrix's
+ * lack list, matrix.c:80-89, and rows whose "identity" column fails the unit
+ * test, the quirk of matrix.c:67-78) get artificial columns appended and are
+ * solved by the two-phase method (default) or Big-M (LPG_ARTIFICIAL=bigm),
+ * the two choices the reference's menu offers (simplex.c:45-55).
+ * Returns 1 (valid) on success, 0 otherwise. */
 short int LPGSolveSMatrix(SimplexMatrix *mx, double constant, double zcoef, short int *inverted) {
-    const int64_t m = (int64_t) mx->basicLen, nc = (int64_t) mx->ofLen + 1;
+    const int64_t m = (int64_t) mx->basicLen, nc0 = (int64_t) mx->ofLen + 1;
     size_t i, j;
     short int valid = 0;
+    int64_t *basis = (int64_t *) calloc((size_t) m, sizeof(int64_t));
+    int64_t nlack = 0;
+    for (i = 0; i < (size_t) m; i++) {
+        for (j = 0; j < mx->ofLen; j++)
+            if (mx->basicVars[i] == mx->varNames[j]) basis[i] = (int64_t) j + 1;
+        if (basis[i]) {   /* keep it only if it is a true unit column */
+            size_t q;
+            for (q = 0; q < (size_t) m; q++)
+                if (Decimalize(*mx->cMatrix[q][basis[i]]) != (q == i ? 1.0 : 0.0)) basis[i] = 0;
+        }
+        if (!basis[i]) nlack++;
+    }
+    const int64_t nc = nc0 + nlack;                 /* artificials appended after the original columns */
     double *rows = (double *) calloc((size_t) (m * nc), sizeof(double));
     double *cost = (double *) calloc((size_t) nc, sizeof(double));
     double *xB = (double *) calloc((size_t) m, sizeof(double));
     double *x = (double *) calloc((size_t) nc, sizeof(double));
-    int64_t *basis = (int64_t *) calloc((size_t) m, sizeof(int64_t));
     lpg_ctx *ctx = NULL;
-    for (i = 0; i < (size_t) m; i++)
-        for (j = 0; j < (size_t) nc; j++)
-            rows[i * nc + j] = Decimalize(*mx->cMatrix[i][j]);
-    for (j = 0; j < mx->ofLen; j++) cost[j] = Decimalize(*mx->ofCosts[j]);
+    int64_t a = nc0;
     for (i = 0; i < (size_t) m; i++) {
-        for (j = 0; j < mx->ofLen; j++)
-            if (mx->basicVars[i] == mx->varNames[j]) basis[i] = (int64_t) j + 1;
-        /* CreateSMatrix's identity test (matrix.c:67-78) can accept a non-unit
-         * column such as (3/2, 1/2); the pivot loop needs a canonical basis. */
-        for (j = 0; j < (size_t) m; j++)
-            if (basis[i] == 0 || rows[j * nc + basis[i]] != (i == j ? 1.0 : 0.0)) {
-                printf("WARNING: basic column of row %zu is not a unit column; artificial variables are needed.\n", i);
-                goto out;
-            }
+        for (j = 0; j < (size_t) nc0; j++)
+            rows[i * nc + j] = Decimalize(*mx->cMatrix[i][j]);
+        if (!basis[i]) {
+            rows[i * nc + a] = 1.0;
+            basis[i] = a++;
+        }
     }
+    for (j = 0; j < mx->ofLen; j++) cost[j] = Decimalize(*mx->ofCosts[j]);
+    const char *method = getenv("LPG_ARTIFICIAL");
+    const int bigm = nlack > 0 && method && strcmp(method, "bigm") == 0;
     int rc;
     lpg_result res;
-    if ((rc = lpg_create(&ctx, 0, m, nc, 0)) != 0 || (rc = lpg_load_rows(ctx, 0, m, rows, nc)) != 0 ||
-        (rc = lpg_set_basis(ctx, basis)) != 0 || (rc = lpg_set_objective(ctx, cost)) != 0 ||
-        (rc = lpg_solve(ctx, (int64_t) 1 << 40, LPG_RULE_DANTZIG, &res)) != 0 ||
-        (rc = lpg_get_column0(ctx, xB)) != 0 || (rc = lpg_get_basis(ctx, basis)) != 0) {
+    if ((rc = lpg_create(&ctx, 0, m, nc, bigm ? LPG_FLAG_BIG_M : 0)) != 0 ||
+        (rc = lpg_load_rows(ctx, 0, m, rows, nc)) != 0 || (rc = lpg_set_basis(ctx, basis)) != 0) {
         printf("ERROR: device simplex failed: %s\n", lpg_last_error(ctx));
         goto out;
     }
-    printf("\n---------------\n> Device Simplex (gfx950, lpg)\n\n");
+    if (nlack == 0)
+        rc = lpg_set_objective(ctx, cost) || lpg_solve(ctx, (int64_t) 1 << 40, LPG_RULE_DANTZIG, &res);
+    else if (bigm)
+        rc = lpg_solve_big_m(ctx, nc0, cost, (int64_t) 1 << 40, LPG_RULE_DANTZIG, &res);
+    else
+        rc = lpg_solve_two_phase(ctx, nc0, cost, (int64_t) 1 << 40, LPG_RULE_DANTZIG, &res);
+    if (rc != 0 || lpg_get_column0(ctx, xB) != 0 || lpg_get_basis(ctx, basis) != 0) {
+        printf("ERROR: device simplex failed: %s\n", lpg_last_error(ctx));
+        goto out;
+    }
+    printf("\n---------------\n> Device Simplex (gfx950, lpg)%s\n\n",
+           nlack == 0 ? "" : (bigm ? ", Big-M (symbolic M)" : ", two-phase"));
     if (res.status == LPG_UNBOUNDED) {
         printf("The LP is UNBOUNDED (after %lld pivots).\n", (long long) res.pivots);
+        valid = 1;
+        goto out;
+    }
+    if (res.status == LPG_INFEASIBLE) {
+        printf("The LP is INFEASIBLE (after %lld pivots).\n", (long long) res.pivots);
         valid = 1;
         goto out;
     }
@@ -125,7 +156,7 @@ SimplexMatrix __wrap_CreateSMatrix(LPModel *model, size_t **lack, short int *val
             constant += Decimalize(model->objective.right[j]->coefficient);
     const double zcoef = Decimalize(model->objective.left[0]->coefficient);
     SimplexMatrix mx = __real_CreateSMatrix(model, lack, valid);
-    if (*valid) {
+    {   /* lacking rows are handled with artificials (the reference then still shows its menu) */
         short int *inv = (short int *) calloc(mx.ofLen + 1, sizeof(short int));
         for (j = 0; j < mx.ofLen && j < model->objective.rightLen; j++)
             inv[j] = model->objective.right[j]->inverted;

@@ -70,3 +70,19 @@ def test_reference_cli_unbounded_and_free_variable():
     assert "UNBOUNDED" in out
     out = _run("a4_free_var.txt", transcripts()["a4_free_var.txt"]["stdin"]).stdout
     assert "UNBOUNDED" in out
+
+
+@needs_bin
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["twophase", "bigm"])
+@pytest.mark.parametrize("name,z", [("a5_lack_row.txt", 6.0), ("a7_identity_quirk.txt", 2.0)])
+def test_reference_cli_artificial_rows(name, z, method):
+    """Rows without a unit column (CreateSMatrix's lack list; the (3/2, 1/2) quirk of
+    matrix.c:67-78) are solved with artificials: the reference's menu choices."""
+    ref = transcripts()[name]
+    env = {**os.environ, "TERM": "dumb", "LPG_ARTIFICIAL": method}
+    out = subprocess.run([BIN, os.path.join("tests", "golden", "lp", name)], input=ref["stdin"], capture_output=True,
+                         text=True, timeout=120, cwd=ROOT, env=env).stdout
+    assert ("Big-M" if method == "bigm" else "two-phase") in out
+    line = next(ln for ln in out.splitlines() if ln.strip().startswith("z = "))
+    assert abs(float(line.split("=")[1]) - z) < 1e-9
