@@ -4,7 +4,10 @@ Workload (BASELINE.json `metric`, config 3): dense synthetic LP m=16384,
 n=32768 (tableau 16385 x 49153 fp64 = 6.44 GB), Dantzig pricing, generated on
 the device (splitmix64, seed 20220518). A "step" is one simplex pivot:
 price (argmin over the reduced-cost row) -> ratio test (min over the entering
-column) -> Gauss-Jordan rank-1 update of the whole tableau.
+column) -> Gauss-Jordan rank-1 update of the whole tableau. By default the
+update is deferred: prep / select evaluate the pending chain for the entries
+they need and k_flush applies each block of K pivots (LPG_DEFER, default 32)
+to the constraint rows in one HBM pass, bitwise identical to K eager updates.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -15,9 +18,11 @@ GPU); per pivot the ranks allgather the ratio candidates and allreduce the
 pivot row over RCCL (strong scaling: the LP is the same for every N).
 
 Rank 0 prints ONE JSON line. `roofline.achieved` = algorithmic bytes of one
-rank-1 update on rank 0 (16 * rows * (N+1): one read + one write of every
-local tableau element) / the update kernel's mean device time, timed with HIP
-events on the engine's own stream over the timed region. `cpu_baseline` =
+launch of the dominant kernel on rank 0 (k_flush: 16 B x local constraint
+rows x columns not skipped, one read + one write of every entry the block
+changes; eager k_update: the same over all rows for one pivot) / its mean
+device time, timed with HIP events on the engine's own stream over the timed
+region. `cpu_baseline` =
 the CPU oracle (oracle/liblpo.so, same pivot rules, OpenMP) on the same LP,
 rank 0 at N=1 only, for a bounded number of pivots; its pivot sequence is
 compared with the GPU's.
@@ -58,6 +63,7 @@ def parse():
     ap.add_argument("--variant", type=int, default=None, help="update-kernel variant (LPG_UPDATE_VARIANT)")
     ap.add_argument("--no-skip", action="store_true", help="update every column (disable column skipping)")
     ap.add_argument("--force-rccl", action="store_true", help="attach a 1-rank RCCL communicator at N=1 (times the exchange)")
+    ap.add_argument("--defer", type=int, default=None, help="pivots per deferred block (LPG_DEFER; 0 = eager updates)")
     return ap.parse_args()
 
 
@@ -110,7 +116,9 @@ def config5(a):
             "data": f"synthetic KM-style degenerate LP with equality rows (splitmix64 seed {SEED}), generated on device",
             "config": {"workload": cfg["name"], "m": m, "n": n, "rule": "bland", "art_first": art_first},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "lpg::k_update",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "lpg::k_flush" if eng.info.defer_k else "lpg::k_update",
+                         "launches_timed": timing.update_count,
                          "algorithmic_bytes_per_launch": touched,
                          "full_tableau_bytes_per_launch": eng.info.bytes_per_pivot, "update_ms_mean": upd_ms},
             "status": lpg.STATUS_NAMES.get(res.status, res.status), "pivots_total": res.pivots,
@@ -138,6 +146,8 @@ def config5(a):
 
 def main():
     a = parse()
+    if a.defer is not None:
+        os.environ["LPG_DEFER"] = str(a.defer)
     if a.config == 5:
         if a.gpus != 1:
             raise SystemExit("config 5 (two-phase) is single-GPU")
@@ -146,6 +156,8 @@ def main():
         return config5(a)
     if a.variant is not None:
         os.environ["LPG_UPDATE_VARIANT"] = str(a.variant)
+    if a.defer is not None:
+        os.environ["LPG_DEFER"] = str(a.defer)
     if a.no_skip:
         os.environ["LPG_NO_SKIP"] = "1"
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,9 +195,11 @@ def main():
     if not live_events:                                # config 2: event-instrumented pass first, while the LP
         eng.set_timing(True)                           # is far from optimal, then the graph-replayed timed region
         eng.get_timing()
-        eng.enqueue(100, lpg.RULE_DANTZIG)
+        eng.enqueue(96, lpg.RULE_DANTZIG)
         eng.sync()
         timing = eng.get_timing()
+        eng.set_timing(False)
+        eng.enqueue(128, lpg.RULE_DANTZIG)             # builds the replayed hipGraph outside the timed region
         before = eng.sync().pivots
     eng.set_timing(live_events)
     if live_events:
@@ -215,9 +229,10 @@ def main():
         dist.all_reduce(dd, op=dist.ReduceOp.MIN)
         done = int(dd.item())
     upd_ms = timing.update_ms / max(timing.update_count, 1)
-    # bytes the update kernel actually read + wrote (skipped all-zero P slices
-    # are not counted); == bytes_per_pivot without skipping
+    # bytes the update / flush kernel actually read + wrote (columns whose
+    # pending P entries are all zero are not counted)
     touched = timing.update_bytes / max(timing.update_count, 1)
+    defer = eng.info.defer_k
     achieved = touched / (upd_ms * 1e-3) / 1e9 if upd_ms > 0 else 0.0
     line = {
         "metric": METRIC,
@@ -236,15 +251,20 @@ def main():
                    "tableau_GB": (m + 1) * (n + m + 1) * 8 / 1e9, "rule": "dantzig",
                    "parallelism": f"row-block x{world}" + (" (RCCL allgather + allreduce per pivot)"
                                                            if world > 1 or a.force_rccl else ""),
+                   "update": (f"deferred blocks of {defer} pivots (one k_flush pass per block)" if defer
+                              else "eager rank-1 update per pivot"),
                    "update_variant": int(os.environ.get("LPG_UPDATE_VARIANT", "-1"))},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "lpg::k_update (Gauss-Jordan rank-1)",
+                     "kernel": (f"lpg::k_flush (Gauss-Jordan, {defer} pending pivots per pass)" if defer
+                                else "lpg::k_update (Gauss-Jordan rank-1)"),
+                     "launches_timed": timing.update_count,
                      "algorithmic_bytes_per_launch": touched,
                      "full_tableau_bytes_per_launch": info.bytes_per_pivot,
                      "column_skipping": not a.no_skip,
                      "update_ms_mean": upd_ms,
-                     "other_ms_mean": timing.select_ms / max(timing.update_count, 1)},
+                     "other_ms_per_pivot": ((elapsed * 1e3 - timing.update_ms) / max(done, 1) if live_events and defer
+                                            else timing.select_ms / max(done if live_events else 96, 1))},
         "status": lpg.STATUS_NAMES.get(res.status, res.status),
         "pivots_total": res.pivots,
         "objective": res.objective,

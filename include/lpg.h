@@ -76,6 +76,15 @@ extern "C" {
 #define LPG_FLAG_NO_LOG  0x1u  /* do not record the (entering, leaving) pivot log */
 #define LPG_FLAG_NO_SKIP 0x2u  /* update every column (no skipping of P[j] == 0 slices) */
 #define LPG_FLAG_BIG_M   0x4u  /* two objective rows: row m = M part, row m+1 = real part (Big-M) */
+#define LPG_FLAG_EAGER   0x8u  /* one rank-1 update pass per pivot instead of deferred (blocked) updates */
+
+/* Deferred updates (default): the constraint rows are brought up to date in
+ * one HBM pass per block of up to LPG_DEFER_MAX pivots (env LPG_DEFER=K picks
+ * K; 0 = eager). Values, pivot sequence and log are bitwise those of eager
+ * updates; every call that reads or replaces the tableau (lpg_get_rows,
+ * lpg_get_column0, lpg_load_rows, lpg_set_basis, lpg_set_objective*, lpg_sync,
+ * lpg_device_sync, the end of lpg_solve) applies the pending block first. */
+#define LPG_DEFER_MAX    64
 
 typedef struct lpg_ctx lpg_ctx;
 
@@ -94,18 +103,22 @@ typedef struct {
     int64_t row0, nrows;        /* this rank's constraint-row block */
     int32_t world, rank, device;
     int32_t nobj;               /* objective rows (1) */
+    int32_t defer_k;            /* pivots per deferred block (0: eager updates) */
+    int32_t pad_;
     double  bytes_per_pivot;    /* algorithmic HBM bytes of one rank-1 update on this rank:
                                    16 * (nrows + nobj) * ncols (one read + one write) */
 } lpg_info_t;
 
 typedef struct {
-    double  update_ms;          /* summed device time of the rank-1 update kernel */
-    double  select_ms;          /* summed device time of pricing + ratio-test kernels */
+    double  update_ms;          /* summed device time of the update kernel (eager: rank-1 update per
+                                   pivot; deferred: the block flush) */
+    double  select_ms;          /* summed device time of pricing + ratio-test kernels (eager mode;
+                                   deferred mode times the flushes only and reports 0) */
     double  comm_ms;            /* summed device time of the collectives */
-    int64_t update_count;       /* update launches timed */
-    double  update_bytes;       /* bytes the update kernels read + wrote (16-byte slices whose
-                                   pivot-row entries are not both zero, x rows, x 2); equals
-                                   update_count * bytes_per_pivot when nothing is skipped */
+    int64_t update_count;       /* update / flush launches timed */
+    double  update_bytes;       /* bytes the update / flush kernels read + wrote (8 B x 2 per tableau
+                                   entry in a column not skipped); eager: equals update_count *
+                                   bytes_per_pivot when nothing is skipped */
 } lpg_timing;
 
 /* Host-staged collectives supplied by the caller (tests, non-RCCL transports).
@@ -167,6 +180,8 @@ int  lpg_solve(lpg_ctx *ctx, int64_t max_pivots, int rule, lpg_result *out);
  * context's stream without any host synchronisation (pivots after the LP
  * finishes are no-ops on the device); lpg_sync waits and reports. */
 int  lpg_enqueue(lpg_ctx *ctx, int64_t npivots, int rule);
+/* Waits for everything enqueued, applies any pending deferred block (so the
+ * tableau is current) and reports. */
 int  lpg_sync(lpg_ctx *ctx, lpg_result *out);
 /* Pre-size the device pivot log for npivots more pivots so that no
  * reallocation (and host synchronisation) happens inside a timed region. */

@@ -22,6 +22,8 @@ GEN_DENSE, GEN_DEGENERATE, GEN_ARTIFICIAL, GEN_DUAL = 0, 1, 2, 3
 FLAG_NO_LOG = 0x1
 FLAG_NO_SKIP = 0x2
 FLAG_BIG_M = 0x4
+FLAG_EAGER = 0x8
+DEFER_MAX = 64
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int64_p = ctypes.POINTER(ctypes.c_int64)
@@ -37,7 +39,8 @@ class Info(ctypes.Structure):
     _fields_ = [("m", ctypes.c_int64), ("ncols", ctypes.c_int64), ("ld", ctypes.c_int64),
                 ("row0", ctypes.c_int64), ("nrows", ctypes.c_int64),
                 ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("nobj", ctypes.c_int32), ("bytes_per_pivot", ctypes.c_double)]
+                ("nobj", ctypes.c_int32), ("defer_k", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("bytes_per_pivot", ctypes.c_double)]
 
 
 class Timing(ctypes.Structure):

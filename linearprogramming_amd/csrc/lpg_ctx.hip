@@ -29,6 +29,7 @@ thread_local char g_err[512];
 
 struct TimingRing {
     std::vector<hipEvent_t> ev;   // 3 per pivot: before prep, before update, after update
+    std::vector<char> upd;        // per pivot: an update / flush kernel ran between marks 1 and 2
     int used = 0;
     double update_ms = 0, select_ms = 0, comm_ms = 0;
     int64_t count = 0;
@@ -65,6 +66,14 @@ struct lpg_ctx {
     int par = 0;                  // parity of the next pivot's slot
     int64_t enq = 0;              // pivots enqueued since the last reset (log bound)
     int update_variant = 0;
+    // deferred (blocked) updates: defer_k pivots per flush (0 = eager)
+    int defer_k = 0;
+    int pend = 0;                 // pivots enqueued since the last flush (host view)
+    int flush_variant = 0;
+    bool capture_block = false;   // capturing a deferred block's pivots (its flush stays outside the graph)
+    double *Pbuf = nullptr, *Cbuf = nullptr;
+    int64_t cs = 0;
+    int64_t *rq = nullptr;
     int skip = 1;                 // column skipping in the update (LPG_FLAG_NO_SKIP turns it off)
     unsigned long long touched_mark = 0;
     // communication
@@ -74,8 +83,8 @@ struct lpg_ctx {
     std::vector<unsigned char> hsend, hrecv;
     // hipGraph of kGraphPivots pivots (starting at parity 0), replayed by
     // enqueue when no communicator and no per-pivot timing is active
-    hipGraphExec_t graph = nullptr;
-    int graph_rule = -1;
+    hipGraphExec_t graph[2] = {nullptr, nullptr};   // by parity of the first pivot
+    int graph_rule[2] = {-1, -1};
     bool use_graphs = true;
     // timing
     bool timing = false;
@@ -177,23 +186,63 @@ static int timing_flush(lpg_ctx *c) {
         float a = 0, b = 0;
         HIPCHK(c, hipEventElapsedTime(&a, t.ev[3 * q], t.ev[3 * q + 1]));
         HIPCHK(c, hipEventElapsedTime(&b, t.ev[3 * q + 1], t.ev[3 * q + 2]));
-        t.select_ms += a;
-        t.update_ms += b;
-        t.count++;
+        if (t.upd[q] != 2) t.select_ms += a;   // 2: a flush-only entry (marks 0 and 1 adjacent)
+        if (t.upd[q]) {
+            t.update_ms += b;
+            t.count++;
+        } else {
+            t.select_ms += b;
+        }
     }
     t.used = 0;
     return 0;
 }
 
-static int timing_mark(lpg_ctx *c, int which) {
+static int timing_mark(lpg_ctx *c, int which, int updated = 1) {
     TimingRing &t = c->tr;
     if (which == 0 && t.used * 3 + 3 > (int)t.ev.size()) {
         int rc = timing_flush(c);
         if (rc) return rc;
     }
     HIPCHK(c, hipEventRecord(t.ev[3 * t.used + which], c->stream));
-    if (which == 2) t.used++;
+    if (which == 2) t.upd[t.used++] = (char)updated;
     return 0;
+}
+
+// ---------------------------------------------------------------------------
+// deferred updates
+// ---------------------------------------------------------------------------
+
+static Defer defer_of(const lpg_ctx *c, int q) {
+    Defer d;
+    d.Pbuf = c->Pbuf;
+    d.Cbuf = c->Cbuf;
+    d.cs = c->cs;
+    d.rq = c->rq;
+    d.basis = c->basis;
+    d.logk = c->logk;
+    d.logr = c->logr;
+    d.q = q;
+    d.on = c->defer_k > 0 ? 1 : 0;
+    return d;
+}
+
+// Apply the pending block (its size on the device is st->npend <= pend).
+// In deferred mode the timing ring brackets exactly this (k_flush +
+// k_flush_pivot_rows + the counter reset).
+static int flush_launch(lpg_ctx *c) {
+    int rc;
+    if (c->timing && ((rc = timing_mark(c, 0)) || (rc = timing_mark(c, 1)))) return rc;
+    if (launch_flush(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, c->skip, c->flush_variant))
+        return fail(c, LPG_ERR_DEVICE, "flush launch failed");
+    c->pend = 0;
+    return c->timing ? timing_mark(c, 2, 2) : 0;
+}
+
+// Bring the constraint rows up to date (no-op in eager mode or with nothing pending).
+static int materialize(lpg_ctx *c) {
+    if (c->defer_k == 0 || c->pend == 0) return 0;
+    return flush_launch(c);
 }
 
 // ---------------------------------------------------------------------------
@@ -206,15 +255,16 @@ static int exchange_candidates(lpg_ctx *c) {
 }
 
 static int bootstrap(lpg_ctx *c, int rule) {
+    int rc = materialize(c);
+    if (rc) return rc;
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
     const Geo g = geo(c);
     if (launch_price(lau(c), g, rule, 0, c->st, 0, c->P, c->C[0], c->pp, c->pc, c->npp))
         return fail(c, LPG_ERR_DEVICE, "price launch failed");
     if (launch_select(lau(c), g, rule, true, c->st, 0, 0, c->P, c->C[1], c->C[0], c->pp, c->npp, c->basis,
-                      c->part, c->nsel, 0, -1, c->pc, c->skip))
+                      c->part, c->nsel, 0, -1, c->pc, c->skip, defer_of(c, 0)))
         return fail(c, LPG_ERR_DEVICE, "select launch failed");
-    int rc = exchange_candidates(c);
-    if (rc) return rc;
+    if ((rc = exchange_candidates(c))) return rc;
     c->par = 0;
     c->booted = true;
     c->boot_rule = rule;
@@ -224,12 +274,13 @@ static int bootstrap(lpg_ctx *c, int rule) {
 // Bootstrap onto a caller-chosen pivot (k, r): no pricing, the ratio test
 // admits only row r (either sign, |T[r][k]| > eps_piv).
 static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
+    int rc = materialize(c);
+    if (rc) return rc;
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
     if (launch_select(lau(c), geo(c), rule, true, c->st, 0, 0, c->P, c->C[1], c->C[0], c->pp, c->npp, c->basis,
-                      c->part, c->nsel, k, r, c->pc, c->skip))
+                      c->part, c->nsel, k, r, c->pc, c->skip, defer_of(c, 0)))
         return fail(c, LPG_ERR_DEVICE, "select launch failed");
-    int rc = exchange_candidates(c);
-    if (rc) return rc;
+    if ((rc = exchange_candidates(c))) return rc;
     c->par = 0;
     c->booted = true;
     c->boot_rule = rule;
@@ -237,37 +288,51 @@ static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
 }
 
 static constexpr int kGraphPivots = 32;
+static constexpr int kDefaultDefer = 32;   // pivots per flush (LPG_DEFER)
 
 static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule);
 
 static void graph_drop(lpg_ctx *c) {
-    if (c->graph) (void)hipGraphExecDestroy(c->graph);
-    c->graph = nullptr;
-    c->graph_rule = -1;
+    for (int p = 0; p < 2; p++) {
+        if (c->graph[p]) (void)hipGraphExecDestroy(c->graph[p]);
+        c->graph[p] = nullptr;
+        c->graph_rule[p] = -1;
+    }
 }
 
-// Capture kGraphPivots pivots starting at parity 0 (the launches read every
-// per-pivot choice from device memory, so one graph serves every replay).
+// Pivots per graph: eager mode kGraphPivots; deferred mode the defer_k pivots
+// of one block (prep + select); the block's flush is launched after each
+// replay, outside the graph, so that it alone can be timed with events.
+static int graph_len(const lpg_ctx *c) { return c->defer_k > 0 ? c->defer_k : kGraphPivots; }
+
+// Capture graph_len pivots starting at the current parity (the launches read
+// every per-pivot choice from device memory, so one graph serves every
+// replay at that parity and block position 0).
 static int graph_build(lpg_ctx *c, int rule) {
-    graph_drop(c);
+    const int par = c->par;
+    if (c->graph[par]) (void)hipGraphExecDestroy(c->graph[par]);
+    c->graph[par] = nullptr;
+    c->graph_rule[par] = -1;
     hipGraph_t g = nullptr;
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    const int par = c->par;
     const int64_t enq = c->enq;
-    c->par = 0;
-    int rc = enqueue_eager(c, kGraphPivots, rule);
+    const int pend = c->pend;
+    c->capture_block = true;
+    int rc = enqueue_eager(c, graph_len(c), rule);
+    c->capture_block = false;
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     c->par = par;
     c->enq = enq;
+    c->pend = pend;
     if (rc) return rc;
     if (e != hipSuccess) return fail(c, LPG_ERR_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(e));
-    e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
+    e = hipGraphInstantiate(&c->graph[par], g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     if (e != hipSuccess) {
-        c->graph = nullptr;
+        c->graph[par] = nullptr;
         return fail(c, LPG_ERR_DEVICE, "hipGraphInstantiate: %s", hipGetErrorString(e));
     }
-    c->graph_rule = rule;
+    c->graph_rule[par] = rule;
     return 0;
 }
 
@@ -276,17 +341,27 @@ static int enqueue(lpg_ctx *c, int64_t npiv, int rule) {
         int rc = bootstrap(c, rule);
         if (rc) return rc;
     }
-    if (!c->use_graphs || c->timing || has_comm(c) || npiv < 2 * kGraphPivots) return enqueue_eager(c, npiv, rule);
+    const int G = graph_len(c);
+    // eager-mode timing brackets every update, which a graph cannot; deferred
+    // timing brackets only the flushes, which stay outside the graph
+    const bool timed = c->timing && c->defer_k == 0;
+    if (!c->use_graphs || timed || has_comm(c) || npiv < 2 * G || (G & 1)) return enqueue_eager(c, npiv, rule);
     int rc;
-    if (c->par == 1) {                       // graphs start at parity 0
-        if ((rc = enqueue_eager(c, 1, rule))) return rc;
-        npiv--;
+    if (c->pend) {                           // finish the open block first
+        const int64_t a = G - c->pend;
+        if ((rc = enqueue_eager(c, a, rule))) return rc;
+        npiv -= a;
     }
-    if (!c->graph || c->graph_rule != rule)
+    const int par = c->par;                  // G is even: every block starts at this parity
+    if (npiv >= G && (!c->graph[par] || c->graph_rule[par] != rule))
         if ((rc = graph_build(c, rule))) return rc;
-    for (; npiv >= kGraphPivots; npiv -= kGraphPivots) {
-        HIPCHK(c, hipGraphLaunch(c->graph, c->stream));
-        c->enq += kGraphPivots;
+    for (; npiv >= G; npiv -= G) {
+        HIPCHK(c, hipGraphLaunch(c->graph[par], c->stream));
+        c->enq += G;
+        if (c->defer_k) {                    // the block's flush
+            c->pend = G;
+            if ((rc = flush_launch(c))) return rc;
+        }
     }
     return enqueue_eager(c, npiv, rule);
 }
@@ -300,23 +375,30 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
     const int ncand = c->nsel * c->world;
     for (int64_t q = 0; q < npiv; q++) {
         const int s = c->par, s1 = s ^ 1;
+        const Defer D = defer_of(c, c->pend);
+        double *P = D.on ? c->Pbuf + (int64_t)c->pend * c->ld : c->P;
         int rc;
-        if (c->timing && (rc = timing_mark(c, 0))) return rc;
-        if (launch_prep(L, g, rule, fuse, c->st, s, c->cand, ncand, c->P, c->C[s], c->pp, c->pc, c->npp))
+        const bool mark = c->timing && !D.on;   // deferred mode times the flushes only
+        if (mark && (rc = timing_mark(c, 0))) return rc;
+        if (launch_prep(L, g, rule, fuse, c->st, s, c->cand, ncand, P, c->C[s], c->pp, c->pc, c->npp, D))
             return fail(c, LPG_ERR_DEVICE, "prep launch failed");
         if (!fuse) {
-            if ((rc = comm_allreduce_sum(c, c->P, (size_t)c->ld))) return rc;
-            if (launch_price(L, g, rule, 1, c->st, s, c->P, c->C[s], c->pp, c->pc, c->npp))
+            if ((rc = comm_allreduce_sum(c, P, (size_t)c->ld))) return rc;
+            if (launch_price(L, g, rule, 1, c->st, s, P, c->C[s], c->pp, c->pc, c->npp, D.on != 0))
                 return fail(c, LPG_ERR_DEVICE, "price launch failed");
         }
-        if (launch_select(L, g, rule, false, c->st, s, s1, c->P, c->C[s], c->C[s1], c->pp, c->npp, c->basis,
-                          c->part, c->nsel, 0, -1, c->pc, c->skip))
+        if (launch_select(L, g, rule, false, c->st, s, s1, P, c->C[s], c->C[s1], c->pp, c->npp, c->basis,
+                          c->part, c->nsel, 0, -1, c->pc, c->skip, D))
             return fail(c, LPG_ERR_DEVICE, "select launch failed");
         if ((rc = exchange_candidates(c))) return rc;
-        if (c->timing && (rc = timing_mark(c, 1))) return rc;
-        if (launch_update(L, g, c->st, s, c->P, c->C[s], c->basis, c->logk, c->logr, c->update_variant, c->skip))
-            return fail(c, LPG_ERR_DEVICE, "update launch failed");
-        if (c->timing && (rc = timing_mark(c, 2))) return rc;
+        if (mark && (rc = timing_mark(c, 1))) return rc;
+        if (!D.on) {
+            if (launch_update(L, g, c->st, s, c->P, c->C[s], c->basis, c->logk, c->logr, c->update_variant, c->skip))
+                return fail(c, LPG_ERR_DEVICE, "update launch failed");
+        } else if (++c->pend == c->defer_k && !c->capture_block) {
+            if ((rc = flush_launch(c))) return rc;
+        }
+        if (mark && (rc = timing_mark(c, 2))) return rc;
         c->par = s1;
         c->enq++;
     }
@@ -351,6 +433,7 @@ static int reset_state(lpg_ctx *c) {
     c->booted = false;
     c->par = 0;
     c->enq = 0;
+    c->pend = 0;
     c->touched_mark = 0;
     return 0;
 }
@@ -427,6 +510,16 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->use_graphs = !(ng && atoi(ng));
     const char *ns = getenv("LPG_NO_SKIP");
     c->skip = ((flags & LPG_FLAG_NO_SKIP) || (ns && atoi(ns))) ? 0 : 1;
+    const char *dk = getenv("LPG_DEFER");
+    c->defer_k = (flags & LPG_FLAG_EAGER) ? 0 : (dk ? atoi(dk) : kDefaultDefer);
+    if (c->defer_k < 0 || c->defer_k > LPG_DEFER_MAX || (c->defer_k && !flush_kmax_supported(c->defer_k))) {
+        fail(c, LPG_ERR_ARG, "LPG_DEFER=%d out of range [0, %d]", c->defer_k, LPG_DEFER_MAX);
+        snprintf(g_err, sizeof g_err, "%s", c->err);
+        delete c;
+        return LPG_ERR_ARG;
+    }
+    const char *fv = getenv("LPG_FLUSH_VARIANT");
+    c->flush_variant = fv ? atoi(fv) : -1;   // -1: launch_flush default
     int rc;
     if ((rc = use_device(c))) { lpg_destroy(c); return rc; }
     const int64_t rows = c->nloc + c->nobj;
@@ -458,6 +551,14 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     else c->cand = c->part;
     ALLOC(c->basis, (size_t)m * sizeof(int64_t));
     ALLOC(c->st, sizeof(DevState));
+    if (c->defer_k > 0) {
+        c->cs = std::max<int64_t>((c->nloc + 63) & ~(int64_t)63, 64);
+        // slots up to the flush kernel's compiled bound (it reads C of every slot)
+        const int64_t slots = flush_kmax_supported(c->defer_k);
+        ALLOC(c->Pbuf, (size_t)slots * c->ld * sizeof(double));
+        ALLOC(c->Cbuf, (size_t)slots * c->cs * sizeof(double));
+        ALLOC(c->rq, (size_t)slots * sizeof(int64_t));
+    }
 #undef ALLOC
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -468,7 +569,8 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->own_stream = true;
     if (hipMemset(c->T, 0, (size_t)rows * c->ld * sizeof(double)) != hipSuccess ||
         hipMemset(c->P, 0, (size_t)c->ld * sizeof(double)) != hipSuccess ||
-        hipMemset(c->basis, 0, (size_t)m * sizeof(int64_t)) != hipSuccess) {
+        hipMemset(c->basis, 0, (size_t)m * sizeof(int64_t)) != hipSuccess ||
+        (c->Cbuf && hipMemset(c->Cbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->cs * sizeof(double)) != hipSuccess)) {
         fail(c, LPG_ERR_DEVICE, "hipMemset failed");
         lpg_destroy(c);
         return LPG_ERR_DEVICE;
@@ -525,7 +627,8 @@ void lpg_destroy(lpg_ctx *c) {
     if (c->nccl) ncclCommDestroy(c->nccl);
     for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
-    void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st};
+    void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
+                    c->Pbuf, c->Cbuf, c->rq};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -543,6 +646,8 @@ int lpg_info(const lpg_ctx *c, lpg_info_t *o) {
     o->rank = c->rank;
     o->device = c->device;
     o->nobj = (int32_t)c->nobj;
+    o->defer_k = c->defer_k;
+    o->pad_ = 0;
     o->bytes_per_pivot = 16.0 * (double)(c->nloc + c->nobj) * (double)c->ncols;
     return 0;
 }
@@ -551,7 +656,7 @@ int lpg_load_rows(lpg_ctx *c, int64_t row0, int64_t nrows, const double *rows, i
     if (!c || !rows || row0 < 0 || nrows < 0 || row0 + nrows > c->m + c->nobj || ld < c->ncols)
         return fail(c, LPG_ERR_ARG, "lpg_load_rows: bad arguments");
     int rc;
-    if ((rc = use_device(c))) return rc;
+    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
     // constraint rows inside this rank's block
     const int64_t a = std::max(row0, c->row0), b = std::min(row0 + nrows, c->row0 + c->nloc);
     if (a < b)
@@ -572,7 +677,8 @@ int lpg_set_basis(lpg_ctx *c, const int64_t *basis) {
     for (int64_t i = 0; i < c->m; i++)
         if (basis[i] < 1 || basis[i] >= c->ncols) return fail(c, LPG_ERR_ARG, "basis[%lld] out of range", (long long)i);
     int rc;
-    if ((rc = use_device(c))) return rc;
+    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(c->basis, basis, c->m * sizeof(int64_t), hipMemcpyHostToDevice));
     return reset_state(c);
 }
@@ -592,7 +698,8 @@ int lpg_set_objective_m(lpg_ctx *c, const double *costM) {
 
 static int set_objective_row(lpg_ctx *c, const double *cost, int64_t orow) {
     int rc;
-    if ((rc = use_device(c))) return rc;
+    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     std::vector<int64_t> hb(c->m);
     HIPCHK(c, hipMemcpy(hb.data(), c->basis, c->m * sizeof(int64_t), hipMemcpyDeviceToHost));
     std::vector<double> hcb(std::max<int64_t>(c->nloc, 1));
@@ -669,7 +776,7 @@ int lpg_reserve_log(lpg_ctx *c, int64_t npivots) {
 int lpg_sync(lpg_ctx *c, lpg_result *out) {
     if (!c) return fail(c, LPG_ERR_ARG, "ctx is NULL");
     int rc;
-    if ((rc = use_device(c))) return rc;
+    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
     return read_result(c, out, c->boot_rule);
 }
 
@@ -699,6 +806,7 @@ int lpg_solve(lpg_ctx *c, int64_t max_pivots, int rule, lpg_result *out) {
         if (r.status != LPG_ITER_LIMIT) break;
         batch = std::min<int64_t>(batch * 2, 256);
     }
+    if ((rc = materialize(c))) return rc;
     return read_result(c, out, rule);
 }
 
@@ -821,7 +929,7 @@ int lpg_solve_dual(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
     if (!c || max_pivots < 0) return fail(c, LPG_ERR_ARG, "lpg_solve_dual: bad arguments");
     if (c->world != 1 || has_comm(c)) return fail(c, LPG_ERR_STATE, "lpg_solve_dual: single rank only");
     int rc;
-    if ((rc = use_device(c))) return rc;
+    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
     // the dual simplex starts from a dual-feasible basis: every d_j >= -eps
     std::vector<double> obj(c->ncols);
     if ((rc = lpg_get_rows(c, c->m + c->nobj - 1, 1, obj.data(), c->ncols))) return rc;
@@ -875,7 +983,7 @@ int lpg_get_rows(lpg_ctx *c, int64_t row0, int64_t nrows, double *out, int64_t l
     if (!c || !out || row0 < 0 || nrows < 0 || row0 + nrows > c->m + c->nobj || ld < c->ncols)
         return fail(c, LPG_ERR_ARG, "lpg_get_rows: bad arguments");
     int rc;
-    if ((rc = use_device(c))) return rc;
+    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const int64_t a = std::max(row0, c->row0), b = std::min(row0 + nrows, c->row0 + c->nloc);
     if (a < b)
@@ -902,7 +1010,7 @@ int lpg_get_basis(lpg_ctx *c, int64_t *basis) {
 int lpg_get_column0(lpg_ctx *c, double *xB) {
     if (!c || !xB) return fail(c, LPG_ERR_ARG, "xB is NULL");
     int rc;
-    if ((rc = use_device(c))) return rc;
+    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->nloc)
         HIPCHK(c, hipMemcpy2D(xB, sizeof(double), c->T, c->ld * sizeof(double), sizeof(double), c->nloc,
@@ -933,6 +1041,7 @@ int lpg_set_timing(lpg_ctx *c, int enable) {
     if ((rc = use_device(c))) return rc;
     if (enable && c->tr.ev.empty()) {
         c->tr.ev.resize(3 * 1024);
+        c->tr.upd.assign(1024, 0);
         for (auto &e : c->tr.ev) HIPCHK(c, hipEventCreate(&e));
     }
     c->timing = enable != 0;
@@ -946,7 +1055,7 @@ int lpg_get_timing(lpg_ctx *c, lpg_timing *out) {
     if ((rc = timing_flush(c))) return rc;
     unsigned long long touched = 0;
     HIPCHK(c, hipMemcpy(&touched, &c->st->touched, sizeof touched, hipMemcpyDeviceToHost));
-    out->update_bytes = 32.0 * (double)(touched - c->touched_mark);
+    out->update_bytes = 16.0 * (double)(touched - c->touched_mark);
     c->touched_mark = touched;
     out->update_ms = c->tr.update_ms;
     out->select_ms = c->tr.select_ms;
@@ -960,7 +1069,7 @@ int lpg_get_timing(lpg_ctx *c, lpg_timing *out) {
 int lpg_device_sync(lpg_ctx *c) {
     if (!c) return fail(c, LPG_ERR_ARG, "ctx is NULL");
     int rc;
-    if ((rc = use_device(c))) return rc;
+    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
 }

@@ -10,6 +10,16 @@
 //   C[t & 1]      column k_t of T_t (the pivot-column snapshot), written by
 //                 select_{t-1} and read by update_t.
 //   P             the normalised pivot row of T_t, written by prep_t.
+//
+// Deferred (blocked) updates, the default for large tableaus: the constraint
+// rows of T lag behind by up to K pending pivots whose P rows, C columns and
+// pivot rows are kept (Defer); the objective row(s) stay current. Any entry
+// of the current tableau is the per-element chain
+//   x = T_base[i][j];  for q in pending order:
+//       x = (i == r_q) ? P_q[j] : fma(-C_q[i], P_q[j], x)
+// which is, operation for operation, what K eager updates compute; prep
+// evaluates it for the pivot row, select for columns 0 and k, and k_flush
+// applies it to the whole block of constraint rows in one HBM pass.
 #pragma once
 #include <stdint.h>
 
@@ -17,6 +27,9 @@ namespace lpg {
 
 constexpr int kBlock = 256;          // threads per block everywhere (4 waves of 64)
 constexpr int kMaxSelBlocks = 512;   // ratio-test partials per rank
+#ifndef LPG_DEFER_MAX
+#define LPG_DEFER_MAX 64             // include/lpg.h
+#endif
 
 enum : int32_t { RUNNING = 0, OPTIMAL = 1, UNBOUNDED = 2, INFEASIBLE = 3, ITER_LIMIT = 4, NUMERIC = 5 };
 enum : int { RULE_DANTZIG = 0, RULE_BLAND = 1 };
@@ -34,8 +47,21 @@ struct DevState {
     int64_t pivots;           // pivots applied (update kernels that ran)
     int64_t last_k, last_r;
     int64_t logcap;
-    unsigned long long touched;   // 16-byte slices the update read+wrote (column skipping accounting)
+    unsigned long long touched;   // tableau doubles the update / flush read+wrote (column skipping accounting)
     unsigned long long work[2];   // k_update work-item dequeue heads, per pivot parity (reset by k_prep)
+    int64_t npend;                // deferred pivots applied but not yet flushed (prep_t sets q + 1)
+    unsigned long long fwork;     // k_flush work-item dequeue head (reset with npend after each flush)
+};
+
+// Pending-pivot buffers of the deferred update (Defer::on == 0: eager mode).
+struct Defer {
+    double  *Pbuf;            // K x ld: P_q (slot q = q-th pivot since the last flush)
+    double  *Cbuf;            // K x cs: C_q (column-major per pivot, rows 0..nloc-1)
+    int64_t  cs;              // Cbuf pitch (>= nloc)
+    int64_t *rq;              // K: local pivot row of pivot q, -1 on a non-owner rank
+    int64_t *basis, *logk, *logr;   // bookkeeping done by prep_t in deferred mode
+    int      q;               // pending index of this pivot
+    int      on;
 };
 
 // Ratio-test candidate: lexicographic (theta, key); row < 0 = none.
@@ -79,13 +105,17 @@ int launch_generate(const Launch &L, const Geo &g, int64_t n, uint64_t seed, int
 int launch_objective_chain(const Launch &L, const Geo &g, const double *cb, const double *acc_in, double *acc_out);
 int launch_objective_finish(const Launch &L, const Geo &g, const double *acc, const double *cost, int64_t orow);
 int launch_price(const Launch &L, const Geo &g, int rule, int mode, const DevState *st, int s,
-                 const double *P, const double *Cs, PricePart *pp, int *pc, int npp);
+                 const double *P, const double *Cs, PricePart *pp, int *pc, int npp, bool defer = false);
 int launch_prep(const Launch &L, const Geo &g, int rule, bool fuse_price, DevState *st, int s,
-                const Cand *cand, int ncand, double *P, const double *Cs, PricePart *pp, int *pc, int npp);
+                const Cand *cand, int ncand, double *P, const double *Cs, PricePart *pp, int *pc, int npp,
+                const Defer &D);
 int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState *st, int s, int s1,
                   const double *P, const double *Cs, double *Cs1, const PricePart *pp, int npp,
                   const int64_t *basis, Cand *part, int nsel, int64_t force_k, int64_t force_r,
-                  const int *pc, int skip);
+                  const int *pc, int skip, const Defer &D);
+// Apply the pending pivots (st->npend <= kmax) to constraint rows 0..nloc-1.
+int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant);
+int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0: k too large)
 int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
                   int64_t *basis, int64_t *logk, int64_t *logr, int variant, int skip);
 

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <stddef.h>
+
 #include <algorithm>
 
 #include "lpg_internal.h"
@@ -275,10 +277,10 @@ __device__ __forceinline__ void count_live(int *__restrict__ pc, bool live) {
 }
 
 template <int RULE, int MODE>
-__global__ __launch_bounds__(kBlock) void k_price(const double *__restrict__ T, Geo g,
+__global__ __launch_bounds__(kBlock) void k_price(double *__restrict__ T, Geo g,
                                                   const DevState *__restrict__ st, int s,
                                                   const double *__restrict__ P, const double *__restrict__ Cs,
-                                                  PricePart *__restrict__ pp, int *__restrict__ pc) {
+                                                  PricePart *__restrict__ pp, int *__restrict__ pc, int defer) {
     if (MODE == 1 && st->slot[s].status != RUNNING) return;
     const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t nvec = (g.ncols + 1) / 2;
@@ -296,6 +298,10 @@ __global__ __launch_bounds__(kBlock) void k_price(const double *__restrict__ T, 
             dR.x = fma(cR, p.x, dR.x);
             dR.y = fma(cR, p.y, dR.y);
             live = p.x != 0.0 || p.y != 0.0;
+            if (defer) {   // deferred mode keeps the objective row(s) current
+                *(d2 *)(T + rR * g.ld + 2 * j2) = dR;
+                if (g.nobj == 2) *(d2 *)(T + rM * g.ld + 2 * j2) = dM;
+            }
         }
         price_one<RULE>(best, dM.x, dR.x, 2 * j2, g);
         price_one<RULE>(best, dM.y, dR.y, 2 * j2 + 1, g);
@@ -306,15 +312,16 @@ __global__ __launch_bounds__(kBlock) void k_price(const double *__restrict__ T, 
 }
 
 int launch_price(const Launch &L, const Geo &g, int rule, int mode, const DevState *st, int s,
-                 const double *P, const double *Cs, PricePart *pp, int *pc, int npp) {
+                 const double *P, const double *Cs, PricePart *pp, int *pc, int npp, bool defer) {
     hipStream_t stream = (hipStream_t)L.stream;
     dim3 grid(npp), blk(kBlock);
+    const int d = defer ? 1 : 0;
     if (rule == RULE_BLAND) {
-        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_BLAND, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc);
-        else hipLaunchKernelGGL((k_price<RULE_BLAND, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc);
+        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_BLAND, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d);
+        else hipLaunchKernelGGL((k_price<RULE_BLAND, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d);
     } else {
-        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_DANTZIG, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc);
-        else hipLaunchKernelGGL((k_price<RULE_DANTZIG, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc);
+        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_DANTZIG, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d);
+        else hipLaunchKernelGGL((k_price<RULE_DANTZIG, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -325,11 +332,11 @@ int launch_price(const Launch &L, const Geo &g, int rule, int mode, const DevSta
 // d_{t+1} fused in (it only needs P and the objective row).
 // ------------------------------------------------------------------------
 
-template <int RULE, bool FUSE>
-__global__ __launch_bounds__(kBlock) void k_prep(const double *__restrict__ T, Geo g, DevState *st, int s,
+template <int RULE, bool FUSE, bool DEFER>
+__global__ __launch_bounds__(kBlock) void k_prep(double *__restrict__ T, Geo g, DevState *st, int s,
                                                  const Cand *__restrict__ cand, int ncand,
                                                  double *__restrict__ P, const double *__restrict__ Cs,
-                                                 PricePart *__restrict__ pp, int *__restrict__ pc) {
+                                                 PricePart *__restrict__ pp, int *__restrict__ pc, Defer D) {
     if (st->slot[s].status != RUNNING) return;
     Cand best{0.0, 0.0, 0, -1};
     for (int q = threadIdx.x; q < ncand; q += kBlock) {
@@ -344,13 +351,36 @@ __global__ __launch_bounds__(kBlock) void k_prep(const double *__restrict__ T, G
         }
         return;
     }
+    const int64_t rl = best.row - g.row0;
+    const bool own = rl >= 0 && rl < g.nloc;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->slot[s].r = best.row;
         st->work[s] = 0;   // k_update's dequeue head for this pivot (runs after this kernel)
+        if (DEFER) {       // no per-pivot update kernel: the pivot is booked here
+            const int64_t k = st->slot[s].k;
+            D.rq[D.q] = own ? rl : -1;
+            st->npend = D.q + 1;
+            D.basis[best.row] = k;
+            const int64_t n = st->pivots;
+            if (D.logk && n < st->logcap) {
+                D.logk[n] = k;
+                D.logr[n] = best.row;
+            }
+            st->pivots = n + 1;
+            st->last_k = k;
+            st->last_r = best.row;
+        }
     }
-    const int64_t rl = best.row - g.row0;
-    const bool own = rl >= 0 && rl < g.nloc;
     const double piv = best.piv;   // == T_t[r][k_t] (select_{t-1} computed and stored it)
+    __shared__ double s_c[LPG_DEFER_MAX];
+    __shared__ int64_t s_rq[LPG_DEFER_MAX];
+    if (DEFER && own) {            // the chain's per-pivot scalars, staged once per block
+        for (int q = threadIdx.x; q < D.q; q += kBlock) {
+            s_rq[q] = D.rq[q];
+            s_c[q] = -D.Cbuf[(int64_t)q * D.cs + rl];
+        }
+        __syncthreads();
+    }
 
     const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t nvec = (g.ncols + 1) / 2;
@@ -359,18 +389,39 @@ __global__ __launch_bounds__(kBlock) void k_prep(const double *__restrict__ T, G
     if (j2 < nvec) {
         d2 p = d2{0.0, 0.0};
         if (own) {
-            const d2 t = *(const d2 *)(T + rl * g.ld + 2 * j2);
+            d2 t = *(const d2 *)(T + rl * g.ld + 2 * j2);
+            if (DEFER) {   // row r of the current tableau: the pending chain
+#pragma unroll 8
+                for (int q = 0; q < D.q; q++) {
+                    const d2 pq = *(const d2 *)(D.Pbuf + (int64_t)q * g.ld + 2 * j2);
+                    if (s_rq[q] == rl) {
+                        t = pq;
+                    } else {
+                        const double c = s_c[q];
+                        t.x = fma(c, pq.x, t.x);
+                        t.y = fma(c, pq.y, t.y);
+                    }
+                }
+            }
             p.x = t.x / piv;
             p.y = t.y / piv;
         }
         *(d2 *)(P + 2 * j2) = p;
         if (FUSE) {
             const int64_t rM = g.nloc, rR = g.nloc + g.nobj - 1;
-            const d2 dM = *(const d2 *)(T + rM * g.ld + 2 * j2);
-            const d2 dR = *(const d2 *)(T + rR * g.ld + 2 * j2);
+            d2 dM = *(const d2 *)(T + rM * g.ld + 2 * j2);
+            d2 dR = *(const d2 *)(T + rR * g.ld + 2 * j2);
             const double cM = -Cs[rM], cR = -Cs[rR];
-            price_one<RULE>(pbest, fma(cM, p.x, dM.x), fma(cR, p.x, dR.x), 2 * j2, g);
-            price_one<RULE>(pbest, fma(cM, p.y, dM.y), fma(cR, p.y, dR.y), 2 * j2 + 1, g);
+            dM.x = fma(cM, p.x, dM.x);
+            dM.y = fma(cM, p.y, dM.y);
+            dR.x = fma(cR, p.x, dR.x);
+            dR.y = fma(cR, p.y, dR.y);
+            if (DEFER) {   // the objective row(s) stay current
+                *(d2 *)(T + rR * g.ld + 2 * j2) = dR;
+                if (g.nobj == 2) *(d2 *)(T + rM * g.ld + 2 * j2) = dM;
+            }
+            price_one<RULE>(pbest, dM.x, dR.x, 2 * j2, g);
+            price_one<RULE>(pbest, dM.y, dR.y, 2 * j2 + 1, g);
             live = p.x != 0.0 || p.y != 0.0;
         }
     }
@@ -382,16 +433,19 @@ __global__ __launch_bounds__(kBlock) void k_prep(const double *__restrict__ T, G
 }
 
 int launch_prep(const Launch &L, const Geo &g, int rule, bool fuse, DevState *st, int s, const Cand *cand,
-                int ncand, double *P, const double *Cs, PricePart *pp, int *pc, int npp) {
+                int ncand, double *P, const double *Cs, PricePart *pp, int *pc, int npp, const Defer &D) {
     hipStream_t stream = (hipStream_t)L.stream;
     dim3 grid(npp), blk(kBlock);
+#define LPG_PREP(R, F, DF) \
+    hipLaunchKernelGGL((k_prep<R, F, DF>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp, pc, D)
     if (rule == RULE_BLAND) {
-        if (fuse) hipLaunchKernelGGL((k_prep<RULE_BLAND, true>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp, pc);
-        else hipLaunchKernelGGL((k_prep<RULE_BLAND, false>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp, pc);
+        if (D.on) { if (fuse) LPG_PREP(RULE_BLAND, true, true); else LPG_PREP(RULE_BLAND, false, true); }
+        else { if (fuse) LPG_PREP(RULE_BLAND, true, false); else LPG_PREP(RULE_BLAND, false, false); }
     } else {
-        if (fuse) hipLaunchKernelGGL((k_prep<RULE_DANTZIG, true>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp, pc);
-        else hipLaunchKernelGGL((k_prep<RULE_DANTZIG, false>), grid, blk, 0, stream, g.T, g, st, s, cand, ncand, P, Cs, pp, pc);
+        if (D.on) { if (fuse) LPG_PREP(RULE_DANTZIG, true, true); else LPG_PREP(RULE_DANTZIG, false, true); }
+        else { if (fuse) LPG_PREP(RULE_DANTZIG, true, false); else LPG_PREP(RULE_DANTZIG, false, false); }
     }
+#undef LPG_PREP
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -403,14 +457,14 @@ int launch_prep(const Launch &L, const Geo &g, int rule, bool fuse, DevState *st
 // FIRST: bootstrap on the tableau as loaded (no pending pivot).
 // ------------------------------------------------------------------------
 
-template <int RULE, bool FIRST>
+template <int RULE, bool FIRST, bool DEFER>
 __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T, Geo g, DevState *st, int s,
                                                    int s1, const double *__restrict__ P,
                                                    const double *__restrict__ Cs, double *__restrict__ Cs1,
                                                    const PricePart *__restrict__ pp, int npp,
                                                    const int64_t *__restrict__ basis, Cand *__restrict__ part,
                                                    int64_t force_k, int64_t force_r,
-                                                   const int *__restrict__ pc, int skip) {
+                                                   const int *__restrict__ pc, int skip, Defer D) {
     Slot *dst = &st->slot[s1];
     if (!FIRST) {
         const int32_t stt = st->slot[s].status;
@@ -423,7 +477,12 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
             return;
         }
     }
-    if (!FIRST && blockIdx.x == 0) {
+    if (DEFER && !FIRST) {
+        // pivot t is pending: keep its column C_t for the chain and the flush
+        for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < g.nloc; i += (int64_t)gridDim.x * kBlock)
+            D.Cbuf[(int64_t)D.q * D.cs + i] = Cs[i];
+    }
+    if (!FIRST && !DEFER && blockIdx.x == 0) {
         // the update of this pivot (next on the stream) touches the live
         // slices of P (all slices without column skipping) in every row
         const int64_t nvec = (g.ncols + 1) / 2;
@@ -440,7 +499,7 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
         if (threadIdx.x == 0) {
             int64_t tot = 0;
             for (int w = 0; w < kBlock / 64; w++) tot += wsum[w];
-            st->touched += (unsigned long long)tot * (unsigned long long)(g.nloc + g.nobj);
+            st->touched += 2ull * (unsigned long long)tot * (unsigned long long)(g.nloc + g.nobj);
         }
     }
     PricePart pb{0.0, -1, 0, 0};
@@ -477,6 +536,17 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
         p0 = P[0];
         pk = P[kn];
     }
+    __shared__ double s_p0[LPG_DEFER_MAX + 1], s_pk[LPG_DEFER_MAX + 1];
+    __shared__ int64_t s_rq[LPG_DEFER_MAX + 1];
+    if (DEFER && !FIRST) {          // the chain's per-pivot scalars, staged once per block
+        for (int q = threadIdx.x; q <= D.q; q += kBlock) {
+            const double *Pq = D.Pbuf + (int64_t)q * g.ld;
+            s_p0[q] = Pq[0];
+            s_pk[q] = Pq[kn];
+            s_rq[q] = D.rq[q];
+        }
+        __syncthreads();
+    }
     const int64_t nrows = g.nloc + g.nobj;
     Cand best{0.0, 0.0, 0, -1};
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock) {
@@ -486,6 +556,33 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
         if (FIRST) {
             b = ob;
             a = oa;
+        } else if (DEFER) {
+            if (i >= g.nloc) {          // objective rows are current (prep / price wrote d_{t+1})
+                b = ob;
+                a = oa;
+            } else {                    // columns 0 and k_{t+1}: chain over pivots 0..q
+                b = ob;
+                a = oa;
+#pragma unroll 8
+                for (int q = 0; q < D.q; q++) {
+                    const double c = -D.Cbuf[(int64_t)q * D.cs + i];
+                    if (i == s_rq[q]) {
+                        b = s_p0[q];
+                        a = s_pk[q];
+                    } else {
+                        b = fma(c, s_p0[q], b);
+                        a = fma(c, s_pk[q], a);
+                    }
+                }
+                if (i == s_rq[D.q]) {       // pivot t itself: C_t is Cs
+                    b = s_p0[D.q];
+                    a = s_pk[D.q];
+                } else {
+                    const double c = -Cs[i];
+                    b = fma(c, s_p0[D.q], b);
+                    a = fma(c, s_pk[D.q], a);
+                }
+            }
         } else if (i == rl) {
             b = p0;
             a = pk;
@@ -512,16 +609,20 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
 
 int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState *st, int s, int s1, const double *P,
                   const double *Cs, double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part,
-                  int nsel, int64_t force_k, int64_t force_r, const int *pc, int skip) {
+                  int nsel, int64_t force_k, int64_t force_r, const int *pc, int skip, const Defer &D) {
     hipStream_t stream = (hipStream_t)L.stream;
     dim3 grid(nsel), blk(kBlock);
-#define LPG_SEL(R, F)                                                                                     \
-    hipLaunchKernelGGL((k_select<R, F>), grid, blk, 0, stream, g.T, g, st, s, s1, P, Cs, Cs1, pp, npp, basis, \
-                       part, force_k, force_r, pc, skip)
+#define LPG_SEL(R, F, DF)                                                                                     \
+    hipLaunchKernelGGL((k_select<R, F, DF>), grid, blk, 0, stream, g.T, g, st, s, s1, P, Cs, Cs1, pp, npp, basis, \
+                       part, force_k, force_r, pc, skip, D)
     if (rule == RULE_BLAND) {
-        if (first) LPG_SEL(RULE_BLAND, true); else LPG_SEL(RULE_BLAND, false);
+        if (first) LPG_SEL(RULE_BLAND, true, false);
+        else if (D.on) LPG_SEL(RULE_BLAND, false, true);
+        else LPG_SEL(RULE_BLAND, false, false);
     } else {
-        if (first) LPG_SEL(RULE_DANTZIG, true); else LPG_SEL(RULE_DANTZIG, false);
+        if (first) LPG_SEL(RULE_DANTZIG, true, false);
+        else if (D.on) LPG_SEL(RULE_DANTZIG, false, true);
+        else LPG_SEL(RULE_DANTZIG, false, false);
     }
 #undef LPG_SEL
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -658,7 +759,7 @@ __global__ __launch_bounds__(kBlock) void k_dual_prep(const double *__restrict__
         if (threadIdx.x == 0) {
             int64_t tot = 0;
             for (int w = 0; w < kBlock / 64; w++) tot += wsum[w];
-            st->touched += (unsigned long long)tot * (unsigned long long)(g.nloc + g.nobj);
+            st->touched += 2ull * (unsigned long long)tot * (unsigned long long)(g.nloc + g.nobj);
             st->slot[s].k = k;
             st->slot[s1].status = RUNNING;
             st->slot[s1].k = -1;
@@ -960,6 +1061,424 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
 #undef LPG_UPD
 #undef LPG_UPD_
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------
+// flush (deferred mode, a12 blocked): apply the np pending pivots to the
+// constraint rows 0..nloc-1 in ONE read-modify-write pass over HBM instead
+// of np passes. Work item = (256-column tile, strip of SR rows). Each lane
+// owns one column j and keeps P_0[j] .. P_{np-1}[j] in VGPRs for the whole
+// strip; the multipliers C_q[i] are wave-uniform and come through the scalar
+// cache (Cbuf is column-major per pivot, so C_q[i..i+RU) is one scalar load).
+// Per element the np fma run in pending order — bit for bit what np eager
+// updates compute; the (at most np) pivot rows, whose chain restarts at
+// x = P_q[j], are rewritten by k_flush_pivot_rows right after. Columns whose
+// pending P entries are all zero are skipped (as in k_update). Persistent
+// grid, dynamic dequeue (st->fwork), RU rows of loads in flight per lane,
+// optionally pipelined.
+// ------------------------------------------------------------------------
+
+template <int RU, bool NT>
+__device__ __forceinline__ void fl_load(double (&x)[RU], const double *col, int64_t i, int64_t ld, bool ok) {
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+        const double *a = col + (i + u) * ld;
+        x[u] = ok ? (NT ? __builtin_nontemporal_load(a) : *a) : 0.0;
+    }
+}
+
+template <int RU, bool NT>
+__device__ __forceinline__ void fl_store(const double (&x)[RU], double *col, int64_t i, int64_t ld, bool ok) {
+    if (!ok) return;
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+        double *a = col + (i + u) * ld;
+        if (NT) __builtin_nontemporal_store(x[u], a);
+        else *a = x[u];
+    }
+}
+
+// The pending chain on RU consecutive rows (pivot rows are rewritten
+// afterwards by k_flush_pivot_rows). sC holds the strip's multipliers,
+// [slot][row], zero for slots >= np (with p[q] == 0 there, fma(-0, 0, x) == x
+// bit for bit, signed zeros and NaN included), so the loop is straight-line.
+// The reads are LDS broadcasts (every lane the same address).
+template <int KMAX, int RU, int SR>
+__device__ __forceinline__ void fl_chain(double (&x)[RU], const double (&p)[KMAX], const double *sC, int lr) {
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) {
+        double c[RU];
+#pragma unroll
+        for (int u = 0; u < RU; u++) c[u] = sC[q * SR + lr + u];
+#pragma unroll
+        for (int u = 0; u < RU; u++) x[u] = fma(-c[u], p[q], x[u]);
+    }
+}
+
+template <int KMAX, int RU, bool NT, bool PIPE, int SR>
+__global__ __launch_bounds__(kBlock) void k_flush(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                  const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
+                                                  int64_t cs, int64_t ntiles, int64_t nitems, int skip) {
+    const int np = (int)st->npend;
+    if (np <= 0) return;
+    const int64_t ld = g.ld;
+    unsigned long long touched = 0;
+    __shared__ int64_t next_item;
+    __shared__ __attribute__((aligned(16))) double sC[KMAX * SR];
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
+        __syncthreads();
+        const int64_t item = next_item;
+        if (item >= nitems) break;
+        const int64_t tile = item % ntiles, strip = item / ntiles;
+        const int64_t i0 = strip * SR;
+        const int64_t i1 = i0 + SR < g.nloc ? i0 + SR : g.nloc;
+        const int64_t j = tile * kBlock + threadIdx.x;
+        bool ok = j < g.ncols;
+        double p[KMAX];
+        bool live = false;
+#pragma unroll
+        for (int q = 0; q < KMAX; q++) {
+            p[q] = (q < np && ok) ? Pbuf[(int64_t)q * ld + j] : 0.0;
+            live = live || p[q] != 0.0;
+        }
+        if (skip) ok = ok && live;   // all pending P zero: the column keeps its values
+        const int cnt = __syncthreads_count(ok);
+        if (cnt == 0) continue;
+        if (threadIdx.x == 0) touched += (unsigned long long)cnt * (unsigned long long)(i1 - i0);
+        // stage C_q[i0 .. i0 + SR) for every slot (zeros past np)
+        for (int e = threadIdx.x; e < KMAX * SR / 2; e += kBlock) {
+            const int q = e / (SR / 2), rr = 2 * (e % (SR / 2));
+            d2 v = d2{0.0, 0.0};
+            if (q < np && i0 + rr < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + i0 + rr);   // i0 + rr + 1 < cs
+            *(d2 *)(sC + q * SR + rr) = v;
+        }
+        __syncthreads();
+        double *col = T + j;
+        int lr = 0;
+        const int nr = (int)(i1 - i0);
+        if (PIPE) {
+            if (lr + RU <= nr) {
+                double x[RU];
+                fl_load<RU, NT>(x, col, i0 + lr, ld, ok);
+                for (;;) {
+                    const bool more = lr + 2 * RU <= nr;
+                    double nx[RU];
+                    if (more) fl_load<RU, NT>(nx, col, i0 + lr + RU, ld, ok);
+                    fl_chain<KMAX, RU, SR>(x, p, sC, lr);
+                    fl_store<RU, NT>(x, col, i0 + lr, ld, ok);
+                    lr += RU;
+                    if (!more) break;
+#pragma unroll
+                    for (int u = 0; u < RU; u++) x[u] = nx[u];
+                }
+            }
+        } else {
+            for (; lr + RU <= nr; lr += RU) {
+                double x[RU];
+                fl_load<RU, NT>(x, col, i0 + lr, ld, ok);
+                fl_chain<KMAX, RU, SR>(x, p, sC, lr);
+                fl_store<RU, NT>(x, col, i0 + lr, ld, ok);
+            }
+        }
+        for (; lr < nr; lr++) {      // tail rows of the last strip
+            double x[1];
+            fl_load<1, NT>(x, col, i0 + lr, ld, ok);
+            fl_chain<KMAX, 1, SR>(x, p, sC, lr);
+            fl_store<1, NT>(x, col, i0 + lr, ld, ok);
+        }
+    }
+    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
+}
+
+// ------------------------------------------------------------------------
+// k_flushm: the flush on the matrix cores. A block of np pending pivots is
+// the rank-np update T -= C (rows x np) * P (np x cols) evaluated in pending
+// order per element, and v_mfma_f64_16x16x4_f64 computes
+//   D[i][j] = fma(A[i][3], B[3][j], fma(A[i][2], B[2][j], fma(A[i][1], B[1][j],
+//             fma(A[i][0], B[0][j], C[i][j]))))
+// bit for bit (tools/mfma_f64_probe.hip, profiles/r01_mfma_f64_probe.log:
+// random, subnormal, signed-zero and inf/nan operands), i.e. four steps of
+// the eager chain with A = -C_q[i], B = P_q[j]. K/4 chained MFMAs per 16x16
+// tile therefore reproduce K eager updates exactly, with no LDS broadcast of
+// C and no per-element VALU work. Slots q >= np use A = -0, B = +0
+// (x + -0 == x).
+//
+// Wave tile: 16 rows x 32*NPAIR columns. Lane l owns column pair
+// 2*(l & 15) (+32 pp) and rows (l >> 4) + 4r, r = 0..3: one 16-byte load per
+// (pair, r), whose .x / .y halves are the accumulators of the even-column and
+// odd-column MFMA tiles (D layout: col = l & 15, row = (l >> 4) + 4r). The
+// B fragments (P_q[j], q = 4g + (l >> 4)) stay in VGPRs for the whole strip;
+// the A fragments (-C_q[i + (l & 15)]) are loaded per 16-row step. The next
+// step's tableau loads are issued before the current step's MFMAs.
+// ------------------------------------------------------------------------
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+template <int KMAX, int NPAIR, bool NT, int SR>
+__global__ __launch_bounds__(kBlock) void k_flushm(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                   const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
+                                                   int64_t cs, int64_t ntiles, int64_t nitems, int skip) {
+    constexpr int G = KMAX / 4;             // MFMA k-steps
+    constexpr int WC = 32 * NPAIR;          // columns per wave
+    constexpr int64_t strip_rows = SR;
+    __shared__ __attribute__((aligned(16))) double sC[KMAX * SR];   // the strip's C, [slot][row]
+    const int np = (int)st->npend;
+    if (np <= 0) return;
+    const int64_t ld = g.ld;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lc = lane & 15, lk = lane >> 4;
+    unsigned long long touched = 0;
+    __shared__ int64_t next_item;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
+        __syncthreads();
+        const int64_t item = next_item;
+        if (item >= nitems) break;
+        const int64_t tile = item % ntiles, strip = item / ntiles;
+        const int64_t i0 = strip * strip_rows;
+        const int64_t i1 = i0 + strip_rows < g.nloc ? i0 + strip_rows : g.nloc;
+        const int64_t c0 = tile * (4 * WC) + wave * WC;
+        // B fragments and column liveness
+        double b[NPAIR][2][G];
+        bool ok[NPAIR];
+        int nlive = 0;
+#pragma unroll
+        for (int pp = 0; pp < NPAIR; pp++) {
+            const int64_t col = c0 + 32 * pp + 2 * lc;
+            const bool in = col < g.ncols;     // col even, ld even: col + 1 < ld
+            bool live = false;
+#pragma unroll
+            for (int gq = 0; gq < G; gq++) {
+                const int q = 4 * gq + lk;
+                d2 v = d2{0.0, 0.0};
+                if (in && q < np) v = *(const d2 *)(Pbuf + (int64_t)q * ld + col);
+                b[pp][0][gq] = v.x;
+                b[pp][1][gq] = v.y;
+                live = live || v.x != 0.0 || v.y != 0.0;
+            }
+            // a column pair is live if any of its P entries over all slots is
+            // non-zero: OR over the 4 lanes holding its k-slices
+            live = __shfl_xor((int)live, 16, 64) | (int)live;
+            live = __shfl_xor((int)live, 32, 64) | (int)live;
+            ok[pp] = in && (!skip || live);
+            nlive += ok[pp] ? (col + 1 < g.ncols ? 2 : 1) : 0;
+        }
+        const int cnt = __syncthreads_count(nlive > 0);
+        if (cnt == 0) continue;
+        {   // touched doubles: each pair counted once (by its lk == 0 lane)
+            int mine = lk == 0 ? nlive : 0;
+            for (int mask = 32; mask > 0; mask >>= 1) mine += __shfl_xor(mine, mask, 64);
+            __shared__ int wsum[kBlock / 64];
+            if (lane == 0) wsum[wave] = mine;
+            __syncthreads();
+            if (threadIdx.x == 0)
+                touched += (unsigned long long)(wsum[0] + wsum[1] + wsum[2] + wsum[3]) * (unsigned long long)(i1 - i0);
+        }
+        // stage C_q[i0 .. i0 + SR) for every slot (zeros past np and past i1: A = -0 there)
+        for (int e = threadIdx.x; e < KMAX * SR / 2; e += kBlock) {
+            const int q = e / (SR / 2), rr = 2 * (e % (SR / 2));
+            d2 v = d2{0.0, 0.0};
+            if (q < np && i0 + rr < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + i0 + rr);   // i0 + rr + 1 < cs
+            *(d2 *)(sC + q * SR + rr) = v;
+        }
+        __syncthreads();
+        d2 t[NPAIR][4];
+        auto load = [&](d2 (&x)[NPAIR][4], int64_t i) {
+#pragma unroll
+            for (int pp = 0; pp < NPAIR; pp++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = i + lk + 4 * r;
+                    const d2 *a = (const d2 *)(T + row * ld + c0 + 32 * pp + 2 * lc);
+                    x[pp][r] = (ok[pp] && row < i1) ? (NT ? __builtin_nontemporal_load(a) : *a) : d2{0.0, 0.0};
+                }
+        };
+        int64_t i = i0;
+        load(t, i);
+        for (;;) {
+            const bool more = i + 16 < i1;
+            d2 tn[NPAIR][4];
+            if (more) load(tn, i + 16);
+            double a[G];
+            const int lr = (int)(i - i0) + lc;
+#pragma unroll
+            for (int gq = 0; gq < G; gq++) a[gq] = -sC[(4 * gq + lk) * SR + lr];
+#pragma unroll
+            for (int pp = 0; pp < NPAIR; pp++) {
+                d4 ae = d4{t[pp][0].x, t[pp][1].x, t[pp][2].x, t[pp][3].x};
+                d4 ao = d4{t[pp][0].y, t[pp][1].y, t[pp][2].y, t[pp][3].y};
+#pragma unroll
+                for (int gq = 0; gq < G; gq++) {
+                    ae = __builtin_amdgcn_mfma_f64_16x16x4f64(a[gq], b[pp][0][gq], ae, 0, 0, 0);
+                    ao = __builtin_amdgcn_mfma_f64_16x16x4f64(a[gq], b[pp][1][gq], ao, 0, 0, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = i + lk + 4 * r;
+                    if (ok[pp] && row < i1) {
+                        d2 *dst = (d2 *)(T + row * ld + c0 + 32 * pp + 2 * lc);
+                        const d2 v = d2{ae[r], ao[r]};
+                        if (NT) __builtin_nontemporal_store(v, dst);
+                        else *dst = v;
+                    }
+                }
+            }
+            if (!more) break;
+            i += 16;
+#pragma unroll
+            for (int pp = 0; pp < NPAIR; pp++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) t[pp][r] = tn[pp][r];
+        }
+    }
+    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
+}
+
+// The pivot rows of the block, after k_flush: row r_q (last occurrence q in
+// the block) = P_q, continued by the chain of the later pivots. These values
+// do not depend on T_base, so the rows k_flush wrote without the replacement
+// are simply overwritten. grid: (column tiles of 256, KMAX slots).
+__global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict__ T, Geo g,
+                                                             const DevState *__restrict__ st,
+                                                             const double *__restrict__ Pbuf,
+                                                             const double *__restrict__ Cbuf, int64_t cs,
+                                                             const int64_t *__restrict__ rq) {
+    const int np = (int)st->npend;
+    const int q = blockIdx.y;
+    if (q >= np) return;
+    const int64_t r = rq[q];
+    if (r < 0) return;                                  // pivot row on another rank
+    for (int q2 = q + 1; q2 < np; q2++)
+        if (rq[q2] == r) return;                        // a later pivot replaces this row again
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= g.ncols) return;
+    double x = Pbuf[(int64_t)q * g.ld + j];
+    for (int q2 = q + 1; q2 < np; q2++) x = fma(-Cbuf[(int64_t)q2 * cs + r], Pbuf[(int64_t)q2 * g.ld + j], x);
+    T[r * g.ld + j] = x;
+}
+
+struct FlushCfg {
+    int mfma;         // 1: k_flushm (matrix cores), 0: k_flush (VALU fma, C through LDS)
+    int ru;           // VALU: rows per batch; MFMA: column pairs per wave (NPAIR)
+    bool nt, pipe;
+    int strip;        // rows per work item (VALU: compile-time LDS tile of C)
+    int per_cu;       // persistent blocks per CU
+};
+
+// Flush variant table (LPG_FLUSH_VARIANT); every variant is bit-identical.
+static const FlushCfg kFlushCfgs[] = {
+    {0, 8, true, true, 64, 4},      // 0
+    {0, 8, true, false, 64, 4},     // 1
+    {0, 4, true, true, 64, 4},      // 2
+    {0, 8, false, true, 64, 4},     // 3
+    {0, 8, true, true, 32, 4},      // 4
+    {0, 8, true, true, 128, 2},     // 5
+    {0, 16, true, false, 64, 4},    // 6
+    {0, 4, true, false, 32, 8},     // 7
+    {1, 1, true, true, 128, 4},     // 8  MFMA, 32 columns per wave
+    {1, 2, true, true, 128, 4},     // 9  MFMA, 64 columns per wave
+    {1, 1, false, true, 64, 8},     // 10
+    {1, 1, true, true, 64, 8},      // 11
+    {1, 1, true, true, 32, 8},      // 12
+    {1, 1, true, true, 32, 4},      // 13
+};
+constexpr int kNumFlushCfgs = sizeof(kFlushCfgs) / sizeof(kFlushCfgs[0]);
+constexpr int kDefaultFlushCfg = 8;
+
+int flush_kmax_supported(int k) {
+    if (k <= 8) return 8;
+    if (k <= 16) return 16;
+    if (k <= 32) return 32;
+    if (k <= 64) return 64;
+    return 0;
+}
+
+static_assert(offsetof(DevState, fwork) == offsetof(DevState, npend) + sizeof(int64_t),
+              "launch_flush clears npend and fwork with one memset");
+
+int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant) {
+    kmax = flush_kmax_supported(kmax);
+    if (!kmax) return -1;
+    if (variant < 0 || variant >= kNumFlushCfgs) variant = kDefaultFlushCfg;
+    FlushCfg cfg = kFlushCfgs[variant];
+    hipStream_t stream = (hipStream_t)L.stream;
+    const int64_t ntiles_p = (g.ncols + kBlock - 1) / kBlock;   // k_flush_pivot_rows column tiles
+    if (cfg.mfma) {
+        const int64_t bcols = 4 * 32 * cfg.ru;
+        const int64_t ntiles = (g.ncols + bcols - 1) / bcols;
+        int strip = cfg.strip;
+        while (strip > 32 && ntiles * ((g.nloc + strip - 1) / strip) < 4096) strip /= 2;
+        while (strip > 32 && kmax * strip * 8 > 32768) strip /= 2;   // LDS tile of C <= 32 KB
+        const int64_t nitems = ntiles * ((g.nloc + strip - 1) / strip);
+        const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * cfg.per_cu);
+        if (nblocks < 1) return 0;
+#define LPG_FM(K, NP, N, S)                                                                                          \
+    hipLaunchKernelGGL((k_flushm<K, NP, N, S>), dim3((unsigned)nblocks), dim3(kBlock), 0, stream, g.T, g, st, D.Pbuf, \
+                       D.Cbuf, D.cs, ntiles, nitems, skip)
+#define LPG_FM_S(K, NP, N)                                              \
+    switch (strip) {                                                    \
+        case 32: LPG_FM(K, NP, N, 32); break;                           \
+        case 64: LPG_FM(K, NP, N, 64); break;                           \
+        default: LPG_FM(K, NP, N, 128); break;                          \
+    }
+#define LPG_FM_K(NP, N)                         \
+    switch (kmax) {                             \
+        case 8: LPG_FM_S(8, NP, N); break;      \
+        case 16: LPG_FM_S(16, NP, N); break;    \
+        case 32: LPG_FM_S(32, NP, N); break;    \
+        default: LPG_FM_S(64, NP, N); break;    \
+    }
+        if (cfg.ru == 2) { if (cfg.nt) LPG_FM_K(2, true) else LPG_FM_K(2, false) }
+        else { if (cfg.nt) LPG_FM_K(1, true) else LPG_FM_K(1, false) }
+#undef LPG_FM_K
+#undef LPG_FM_S
+#undef LPG_FM
+    } else {
+        const int64_t ntiles = ntiles_p;
+        // small tableaus: 32-row strips so that the items fill the chip
+        if (ntiles * ((g.nloc + cfg.strip - 1) / cfg.strip) < 4096) cfg.strip = 32;
+        // the LDS tile is KMAX x strip doubles: keep it within 64 KB
+        while (cfg.strip > 32 && kmax * cfg.strip * 8 > 65536) cfg.strip /= 2;
+        const int64_t nitems = ntiles * ((g.nloc + cfg.strip - 1) / cfg.strip);
+        const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * cfg.per_cu);
+        if (nblocks < 1) return 0;
+        dim3 grid((unsigned)nblocks), blk(kBlock);
+#define LPG_FL(K, R, N, PI, S)                                                                                   \
+    hipLaunchKernelGGL((k_flush<K, R, N, PI, S>), grid, blk, 0, stream, g.T, g, st, D.Pbuf, D.Cbuf, D.cs, ntiles, \
+                       nitems, skip)
+#define LPG_FL_S(K, R, N, PI)                                   \
+    switch (cfg.strip) {                                        \
+        case 32: LPG_FL(K, R, N, PI, 32); break;                \
+        case 64: LPG_FL(K, R, N, PI, 64); break;                \
+        default: LPG_FL(K, R, N, PI, 128); break;               \
+    }
+#define LPG_FL_K(R, N, PI)                       \
+    switch (kmax) {                              \
+        case 8: LPG_FL_S(8, R, N, PI); break;    \
+        case 16: LPG_FL_S(16, R, N, PI); break;  \
+        case 32: LPG_FL_S(32, R, N, PI); break;  \
+        default: LPG_FL_S(64, R, N, PI); break;  \
+    }
+        switch (variant) {
+            case 1: LPG_FL_K(8, true, false); break;
+            case 2: LPG_FL_K(4, true, true); break;
+            case 3: LPG_FL_K(8, false, true); break;
+            case 6: LPG_FL_K(16, true, false); break;
+            case 7: LPG_FL_K(4, true, false); break;
+            default: LPG_FL_K(8, true, true); break;
+        }
+#undef LPG_FL_K
+#undef LPG_FL_S
+#undef LPG_FL
+    }
+    hipLaunchKernelGGL(k_flush_pivot_rows, dim3((unsigned)ntiles_p, (unsigned)kmax), dim3(kBlock), 0, stream, g.T, g, st,
+                       D.Pbuf, D.Cbuf, D.cs, D.rq);
+    if (hipGetLastError() != hipSuccess) return -1;
+    // the pending block is applied: clear it and the dequeue head
+    return hipMemsetAsync(&st->npend, 0, sizeof(int64_t) + sizeof(unsigned long long), stream) == hipSuccess ? 0 : -1;
 }
 
 }  // namespace lpg

@@ -1,0 +1,167 @@
+"""Deferred (blocked) updates vs eager updates and the oracle, bitwise.
+
+In deferred mode the constraint rows lag behind by up to K pending pivots;
+prep / select evaluate the pending chain x = (i == r_q) ? P_q[j] :
+fma(-C_q[i], P_q[j], x) for the entries they need and k_flush applies the
+block in one pass. The operations per tableau entry are exactly the eager
+ones, so every pivot log, basis, objective and whole tableau must equal the
+oracle's (np.array_equal) for any block size K, including blocks cut short by
+a read (lpg_get_rows), by the end of a solve, or by an early stop.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle.lpo import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lpg():
+    import linearprogramming_amd as lpg
+    lpg.load()
+    assert lpg.device_count() >= 1, "no GPU visible"
+    return lpg
+
+
+def _log(x):
+    k, r = x.get_log()
+    return list(zip(k.tolist(), r.tolist()))
+
+
+def _assert_same(e, o, m):
+    assert _log(e) == _log(o)
+    assert np.array_equal(e.get_basis(), o.get_basis())
+    assert np.array_equal(e.get_rows(0, m + 1), o.get_rows())
+
+
+def _engine(lpg, monkeypatch, k, m, ncols, **kw):
+    monkeypatch.setenv("LPG_DEFER", str(k))
+    e = lpg.Engine(m, ncols, **kw)
+    monkeypatch.delenv("LPG_DEFER")
+    return e
+
+
+@pytest.mark.parametrize("k", [0, 1, 2, 3, 8, 16, 31, 32, 64])
+@pytest.mark.parametrize("m,n,seed,kind,rule", [(200, 300, 12, 0, 0), (48, 48, 14, 1, 1), (257, 100, 15, 1, 0)])
+def test_block_sizes_to_optimality(lpg, monkeypatch, k, m, n, seed, kind, rule):
+    e = _engine(lpg, monkeypatch, k, m, n + m + 1)
+    o = Oracle(m, n + m + 1)
+    e.generate(n, seed, kind)
+    o.generate(n, seed, kind)
+    res = e.solve(200_000, rule)
+    ores = o.solve(200_000, rule)
+    assert res.status == ores.status == 1
+    assert res.pivots == ores.pivots > 0 and res.objective == ores.objective
+    _assert_same(e, o, m)
+
+
+@pytest.mark.parametrize("k", [8, 32, 64])
+def test_config2_to_optimality(lpg, monkeypatch, k):
+    m, n = 1024, 2048
+    e = _engine(lpg, monkeypatch, k, m, n + m + 1)
+    o = Oracle(m, n + m + 1, nthreads=8)
+    e.generate(n, 20220518, 0)
+    o.generate(n, 20220518, 0)
+    res = e.solve(200_000, 0)
+    ores = o.solve(200_000, 0)
+    assert res.status == ores.status == 1 and res.pivots == ores.pivots
+    _assert_same(e, o, m)
+
+
+def test_reads_inside_a_block(lpg, monkeypatch):
+    """Reads in the middle of a block flush it; the loop then continues from the
+    flushed tableau and stays on the oracle's path."""
+    m, n = 150, 220
+    e = _engine(lpg, monkeypatch, 32, m, n + m + 1)
+    o = Oracle(m, n + m + 1)
+    e.generate(n, 71, 0)
+    o.generate(n, 71, 0)
+    for step in (5, 1, 13, 32, 40, 3):
+        e.enqueue(step, 0)
+        assert e.get_column0().shape == (m,)           # flushes
+        o.solve(step, 0)
+        _assert_same(e, o, m)
+    res, ores = e.solve(100_000, 0), o.solve(100_000, 0)
+    assert res.pivots == ores.pivots and res.objective == ores.objective
+    _assert_same(e, o, m)
+
+
+def test_enqueue_past_optimal_partial_block(lpg, monkeypatch):
+    """The LP finishes inside a block: the later pivots are device no-ops and the
+    flush applies only the pivots actually taken."""
+    m, n = 40, 60
+    e = _engine(lpg, monkeypatch, 32, m, n + m + 1)
+    o = Oracle(m, n + m + 1)
+    e.generate(n, 21, 0)
+    o.generate(n, 21, 0)
+    ores = o.solve(100_000, 0)
+    e.enqueue(ores.pivots + 45, 0)
+    res = e.sync()
+    assert res.status_name == "OPTIMAL" and res.pivots == ores.pivots
+    _assert_same(e, o, m)
+
+
+@pytest.mark.parametrize("variant", list(range(14)))
+def test_flush_variants_identical(lpg, monkeypatch, variant):
+    monkeypatch.setenv("LPG_FLUSH_VARIANT", str(variant))
+    m, n = 300, 700
+    e = _engine(lpg, monkeypatch, 32, m, n + m + 1)
+    o = Oracle(m, n + m + 1)
+    e.generate(n, 24, 0)
+    o.generate(n, 24, 0)
+    res = e.solve(100, 0)
+    o.solve(100, 0)
+    assert res.pivots == 100
+    _assert_same(e, o, m)
+
+
+def test_flush_accounting(lpg, monkeypatch):
+    """Without column skipping a flush reads and writes every constraint-row entry
+    once: 16 B x m x ncols per flush, one flush per K pivots."""
+    m, n, k = 256, 512, 8
+    monkeypatch.setenv("LPG_NO_SKIP", "1")
+    e = _engine(lpg, monkeypatch, k, m, n + m + 1)
+    e.generate(n, 81, 0)
+    e.set_timing(True)
+    e.get_timing()
+    e.enqueue(32, 0)
+    e.sync()
+    t = e.get_timing()
+    assert t.update_count == 32 // k
+    assert t.update_bytes == t.update_count * 16 * m * (n + m + 1)
+    assert t.update_ms > 0 and t.select_ms == 0      # deferred mode times the flushes only
+
+
+def test_eager_flag(lpg):
+    e = lpg.Engine(64, 64 + 96 + 1, flags=lpg._lib.FLAG_EAGER)
+    o = Oracle(64, 64 + 96 + 1)
+    e.generate(96, 5, 0)
+    o.generate(96, 5, 0)
+    assert e.solve(10_000, 0).pivots == o.solve(10_000, 0).pivots
+    _assert_same(e, o, 64)
+
+
+def test_bad_block_size(lpg, monkeypatch):
+    monkeypatch.setenv("LPG_DEFER", "65")
+    with pytest.raises(lpg.LPGError):
+        lpg.Engine(8, 20)
+
+
+@pytest.mark.parametrize("variant", [7, 8, 9])
+@pytest.mark.parametrize("k", [3, 8, 32, 64])
+@pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1)])
+def test_flush_kernels_block_sizes(lpg, monkeypatch, variant, k, m, n, seed, kind, rule):
+    """VALU (7) and matrix-core (8, 9) flushes at every compiled block bound, to
+    optimality, against the oracle (odd shapes: ragged column tiles and strips)."""
+    monkeypatch.setenv("LPG_FLUSH_VARIANT", str(variant))
+    e = _engine(lpg, monkeypatch, k, m, n + m + 1)
+    o = Oracle(m, n + m + 1)
+    e.generate(n, seed, kind)
+    o.generate(n, seed, kind)
+    res = e.solve(200_000, rule)
+    ores = o.solve(200_000, rule)
+    assert res.status == ores.status == 1 and res.pivots == ores.pivots
+    _assert_same(e, o, m)

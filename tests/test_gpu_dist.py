@@ -86,8 +86,12 @@ def lpg():
     return lpg
 
 
+@pytest.mark.parametrize("defer", [None, "0", "5"])
 @pytest.mark.parametrize("world,m,n,kind,rule", [(2, 96, 160, 0, 0), (3, 101, 77, 0, 0), (2, 64, 64, 1, 1)])
-def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule):
+def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule, defer, monkeypatch):
+    """Row blocks over ranks; default deferred blocks, eager (0) and 5-pivot blocks."""
+    if defer is not None:
+        monkeypatch.setenv("LPG_DEFER", defer)
     seed = 777
     parts = _run_threads(lpg, world, m, n, seed, kind, rule, 5000)
     o = Oracle(m, n + m + 1)

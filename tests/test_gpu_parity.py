@@ -213,6 +213,7 @@ def test_set_objective_general_basis(lpg):
 
 @pytest.mark.parametrize("variant", list(range(25)))
 def test_update_variants_identical(lpg, variant, monkeypatch):
+    monkeypatch.setenv("LPG_DEFER", "0")            # the per-pivot update kernel runs in eager mode
     monkeypatch.setenv("LPG_UPDATE_VARIANT", str(variant))
     m, n = 300, 700
     e, o = _pair(lpg, m, n + m + 1)
@@ -228,7 +229,8 @@ def test_update_variants_identical(lpg, variant, monkeypatch):
 def test_column_skipping_is_value_identical(lpg, m, n, kind, rule, piv, monkeypatch):
     """Skipping slices whose pivot-row entries are zero changes no value (np.array_equal;
     only the sign of a zero may differ) and no decision; the touched-bytes counter is
-    exact without skipping and smaller with it."""
+    exact without skipping and smaller with it (eager per-pivot update)."""
+    monkeypatch.setenv("LPG_DEFER", "0")
     e = lpg.Engine(m, n + m + 1)
     monkeypatch.setenv("LPG_NO_SKIP", "1")
     f = lpg.Engine(m, n + m + 1)
@@ -246,9 +248,12 @@ def test_column_skipping_is_value_identical(lpg, m, n, kind, rule, piv, monkeypa
     assert 0 < te.update_bytes < tf.update_bytes
 
 
-def test_graph_replay_identical(lpg, monkeypatch):
-    """Batches of >= 64 pivots replay a captured hipGraph of 32 pivots; the result
-    must be bitwise the eager launches (LPG_NO_GRAPH=1) and the oracle."""
+@pytest.mark.parametrize("defer", ["0", "32", "8"])
+def test_graph_replay_identical(lpg, defer, monkeypatch):
+    """Batches of >= 2 graph lengths replay a captured hipGraph (32 pivots eager, one
+    block of K pivots + its flush deferred); the result must be bitwise the eager
+    launches (LPG_NO_GRAPH=1) and the oracle."""
+    monkeypatch.setenv("LPG_DEFER", defer)
     m, n = 200, 300
     e = lpg.Engine(m, n + m + 1)
     monkeypatch.setenv("LPG_NO_GRAPH", "1")
@@ -257,7 +262,7 @@ def test_graph_replay_identical(lpg, monkeypatch):
     o = Oracle(m, n + m + 1)
     for x in (e, f, o):
         x.generate(n, 61, 0)
-    e.enqueue(1, 0)            # odd start: the graph path must realign to parity 0
+    e.enqueue(1, 0)            # odd start: a graph per parity; deferred: finish the open block first
     e.enqueue(150, 0)
     r = e.sync()
     f.solve(151, 0)
@@ -267,7 +272,8 @@ def test_graph_replay_identical(lpg, monkeypatch):
     _assert_same(f, o, m)
 
 
-def test_timing_counters(lpg):
+def test_timing_counters(lpg, monkeypatch):
+    monkeypatch.setenv("LPG_DEFER", "0")
     e = lpg.Engine(512, 512 + 1024 + 1)
     e.generate(1024, 25, 0)
     e.set_timing(True)

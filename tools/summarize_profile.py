@@ -5,7 +5,7 @@
 writes
   profiles/rNN_kernel_stats.csv     rocprofv3 --kernel-trace --stats summary (as produced)
   profiles/rNN_pmc.json             per-kernel FETCH_SIZE / WRITE_SIZE means and HBM bytes
-  profiles/pmc_configC.json         update-kernel HBM bytes per launch, read by bench.py
+  profiles/pmc_configC.json         dominant kernel's HBM bytes per launch, read by bench.py
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
 KB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane)
@@ -32,7 +32,7 @@ def _one(pattern):
 
 
 def short(name: str) -> str:
-    for key in ("k_update", "k_select", "k_prep", "k_price", "k_generate", "k_basis_slack", "k_objective"):
+    for key in ("k_flush_pivot_rows", "k_flush", "k_update", "k_select", "k_prep", "k_price", "k_generate", "k_basis_slack", "k_objective"):
         if key in name:
             return key
     return name[:60]
@@ -69,20 +69,27 @@ def main():
         out["FETCH_SIZE"] = counter_means(fetch, "FETCH_SIZE")
     if write:
         out["WRITE_SIZE"] = counter_means(write, "WRITE_SIZE")
+    # dominant kernel: the deferred block flush if it ran, else the eager update
+    kern = "k_flush" if fetch and "k_flush" in out.get("FETCH_SIZE", {}) else "k_update"
+    # FETCH_SIZE correction: x2 for 16-B/lane streaming reads (guide); other widths
+    # are calibrated with tools/hbm_calib3 (--fetch-factor F)
+    ff = float(os.environ.get("FETCH_FACTOR", "2.0"))
+    out["dominant_kernel"] = kern
+    out["fetch_factor"] = ff
     upd = None
-    if fetch and write and "k_update" in out["FETCH_SIZE"] and "k_update" in out["WRITE_SIZE"]:
-        f_kb = out["FETCH_SIZE"]["k_update"]["mean_KB"]
-        w_kb = out["WRITE_SIZE"]["k_update"]["mean_KB"]
-        upd = (2 * f_kb + w_kb) * 1024
-        out["k_update_hbm_bytes_per_launch"] = upd
-        out["k_update_read_bytes"] = 2 * f_kb * 1024
-        out["k_update_write_bytes"] = w_kb * 1024
+    if fetch and write and kern in out["FETCH_SIZE"] and kern in out["WRITE_SIZE"]:
+        f_kb = out["FETCH_SIZE"][kern]["mean_KB"]
+        w_kb = out["WRITE_SIZE"][kern]["mean_KB"]
+        upd = (ff * f_kb + w_kb) * 1024
+        out[f"{kern}_hbm_bytes_per_launch"] = upd
+        out[f"{kern}_read_bytes"] = ff * f_kb * 1024
+        out[f"{kern}_write_bytes"] = w_kb * 1024
     with open(os.path.join(ROOT, "profiles", f"r{rnd:02d}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
     if upd is not None:
         with open(os.path.join(ROOT, "profiles", f"pmc_config{cfg}.json"), "w") as f:
             json.dump({"hbm_bytes_per_launch": upd, "source": f"profiles/r{rnd:02d}_pmc.json",
-                       "kernel": "lpg::k_update"}, f, indent=1)
+                       "kernel": f"lpg::{kern}", "fetch_factor": ff}, f, indent=1)
     print(json.dumps(out, indent=1))
 
 
