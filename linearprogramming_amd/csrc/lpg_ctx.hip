@@ -71,6 +71,7 @@ struct lpg_ctx {
     int pend = 0;                 // pivots enqueued since the last flush (host view)
     int flush_variant = 0;
     bool capture_block = false;   // capturing a deferred block's pivots (its flush stays outside the graph)
+    bool fast_pivot = true;       // deferred single-rank pivots through k_prep_d / k_select_d (LPG_SLOW_PIVOT=1: generic pair)
     double *Pbuf = nullptr, *Cbuf = nullptr;
     int64_t cs = 0;
     int64_t *rq = nullptr;
@@ -380,6 +381,16 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
         int rc;
         const bool mark = c->timing && !D.on;   // deferred mode times the flushes only
         if (mark && (rc = timing_mark(c, 0))) return rc;
+        if (D.on && fuse && c->fast_pivot) {    // deferred, single rank: the prefetching pair
+            if (launch_pivot_d(L, g, rule, c->st, s, s1, c->part, c->nsel, P, c->C[s], c->C[s1], c->pp, c->npp,
+                               c->basis, D))
+                return fail(c, LPG_ERR_DEVICE, "pivot launch failed");
+            if (++c->pend == c->defer_k && !c->capture_block)
+                if ((rc = flush_launch(c))) return rc;
+            c->par = s1;
+            c->enq++;
+            continue;
+        }
         if (launch_prep(L, g, rule, fuse, c->st, s, c->cand, ncand, P, c->C[s], c->pp, c->pc, c->npp, D))
             return fail(c, LPG_ERR_DEVICE, "prep launch failed");
         if (!fuse) {
@@ -518,6 +529,8 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         delete c;
         return LPG_ERR_ARG;
     }
+    const char *sp = getenv("LPG_SLOW_PIVOT");
+    c->fast_pivot = !(sp && atoi(sp));
     const char *fv = getenv("LPG_FLUSH_VARIANT");
     c->flush_variant = fv ? atoi(fv) : -1;   // -1: launch_flush default
     int rc;
@@ -527,6 +540,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->npp = price_blocks(g);
     const int64_t maxloc = (m + world - 1) / world + c->nobj;   // identical on every rank
     c->nsel = (int)std::min<int64_t>((maxloc + kBlock - 1) / kBlock, kMaxSelBlocks);
+    if ((int64_t)c->nsel * kBlock < rows) c->fast_pivot = false;   // k_select_d takes one row per thread
 #define ALLOC(p, bytes)                                                                    \
     do {                                                                                   \
         hipError_t e_ = hipMalloc((void **)&(p), (bytes));                                 \
@@ -1073,5 +1087,10 @@ int lpg_device_sync(lpg_ctx *c) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
 }
+
+#ifdef LPG_PHASES
+// tools/phase_probe.py only (not part of include/lpg.h; absent from liblpg.so)
+int lpg_debug_phases(unsigned long long *out, int reset) { return lpg::debug_phases(out, reset); }
+#endif
 
 }  // extern "C"

@@ -113,6 +113,11 @@ int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState 
                   const double *P, const double *Cs, double *Cs1, const PricePart *pp, int npp,
                   const int64_t *basis, Cand *part, int nsel, int64_t force_k, int64_t force_r,
                   const int *pc, int skip, const Defer &D);
+// One deferred-mode pivot without a communicator: k_prep_d + k_select_d
+// (prefetching forms of prep + select; candidates in and out through part).
+int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, Cand *part, int nsel,
+                   double *P, const double *Cs, double *Cs1, PricePart *pp, int npp, const int64_t *basis,
+                   const Defer &D);
 // Apply the pending pivots (st->npend <= kmax) to constraint rows 0..nloc-1.
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant);
 int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0: k too large)
@@ -123,6 +128,9 @@ int launch_dual_rows(const Launch &L, const Geo &g, Cand *part, int nsel);
 int launch_dual_pivot(const Launch &L, const Geo &g, DevState *st, int s, Cand *part, int nsel, PricePart *pp,
                       int *pc, int npp, int skip, double *P, double *Cs);
 
+#ifdef LPG_PHASES
+int debug_phases(unsigned long long *out, int reset);   // tools/phase_probe.py
+#endif
 int price_blocks(const Geo &g);      // number of pricing partials (= prep / price grid)
 int update_variants();               // entries of the update-kernel variant table
 int update_auto_variant(const Geo &g);   // default variant for this geometry

@@ -100,6 +100,134 @@ __device__ PricePart block_reduce_pp(PricePart p) {
     return b;
 }
 
+// ---- fast block argmins for the deferred pivot kernels -------------------
+// Candidates are ordered by a unique lexicographic key (hi: u64, lo: u32);
+// an invalid candidate is (~0, ~0). Ratio candidates: hi = the bits of
+// theta >= 0 (non-negative doubles order like their bit patterns), lo = the
+// tie key (row or basic column). Pricing partials: hi = cls << 63 | ~bits(v)
+// (v < 0, so ~bits orders most-negative first), lo = j; Bland: hi = 0,
+// lo = j. The minimum key is the same candidate block_reduce_cand /
+// block_reduce_pp pick (a total order, so the reduction tree cannot change
+// the winner). Within a wave: four DPP steps (xor 1, xor 2, half-mirror,
+// mirror) leave each 16-lane row's minimum in every lane of the row, then
+// the four rows through readlane; the winning lane is found by ballot and
+// its payload read with readlane; the four waves meet in LDS (one barrier
+// pair instead of log2(64) LDS permutes per field).
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ bool key_less(uint64_t ah, uint32_t al, uint64_t bh, uint32_t bl) {
+    return ah < bh || (ah == bh && al < bl);
+}
+
+template <int CTRL>
+__device__ __forceinline__ void key_step(uint64_t &h, uint32_t &l) {
+    const uint32_t h0 = dpp32<CTRL>((uint32_t)h), h1 = dpp32<CTRL>((uint32_t)(h >> 32)), l1 = dpp32<CTRL>(l);
+    const uint64_t oh = ((uint64_t)h1 << 32) | h0;
+    if (key_less(oh, l1, h, l)) {
+        h = oh;
+        l = l1;
+    }
+}
+
+__device__ __forceinline__ uint32_t rdl32(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, lane); }
+__device__ __forceinline__ uint64_t rdl64(uint64_t v, int lane) {
+    return ((uint64_t)rdl32((uint32_t)(v >> 32), lane) << 32) | rdl32((uint32_t)v, lane);
+}
+
+// minimum key of the wave, uniform in every lane
+__device__ __forceinline__ void wave_min_key(uint64_t &h, uint32_t &l) {
+    key_step<0xB1>(h, l);    // quad_perm [1,0,3,2]: lane ^ 1
+    key_step<0x4E>(h, l);    // quad_perm [2,3,0,1]: lane ^ 2
+    key_step<0x141>(h, l);   // row_half_mirror: i <-> 7 - i
+    key_step<0x140>(h, l);   // row_mirror: i <-> 15 - i
+    uint64_t bh = rdl64(h, 0);
+    uint32_t bl = rdl32(l, 0);
+#pragma unroll
+    for (int r = 1; r < 4; r++) {
+        const uint64_t rh = rdl64(h, 16 * r);
+        const uint32_t rl = rdl32(l, 16 * r);
+        if (key_less(rh, rl, bh, bl)) {
+            bh = rh;
+            bl = rl;
+        }
+    }
+    h = bh;
+    l = bl;
+}
+
+__device__ __forceinline__ int winner_lane(bool mine) {
+    const unsigned long long m = __ballot(mine);
+    return m ? __ffsll((long long)m) - 1 : -1;
+}
+
+// == block_reduce_cand for candidates with theta >= 0 and unique keys
+__device__ Cand block_argmin_cand(const Cand &c) {
+    const bool valid = c.row >= 0;
+    uint64_t h = valid ? (uint64_t)__double_as_longlong(c.theta) : ~0ull;
+    uint32_t l = valid ? (uint32_t)c.key : ~0u;
+    const uint64_t mh = h;
+    const uint32_t ml = l;
+    wave_min_key(h, l);
+    const int src = winner_lane(valid && mh == h && ml == l);
+    __shared__ Cand sw[kBlock / 64];
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        Cand o{0.0, 0.0, 0, -1};
+        if (src >= 0) {
+            o.theta = __longlong_as_double((long long)h);
+            o.key = (int64_t)l;
+            o.piv = __longlong_as_double((long long)rdl64((uint64_t)__double_as_longlong(c.piv), src));
+            o.row = (int64_t)rdl64((uint64_t)c.row, src);
+        }
+        sw[w] = o;
+    }
+    __syncthreads();
+    Cand b = sw[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / 64; i++)
+        if (cand_better(sw[i], b)) b = sw[i];
+    return b;
+}
+
+// == block_reduce_pp<RULE> for eligible partials (v < 0, unique j)
+template <int RULE>
+__device__ PricePart block_argmin_pp(const PricePart &p) {
+    const bool valid = p.j >= 0;
+    uint64_t h = ~0ull;
+    if (valid)
+        h = RULE == RULE_BLAND ? 0ull
+                               : (((uint64_t)(uint32_t)p.cls << 63) |
+                                  (~(uint64_t)__double_as_longlong(p.v) & 0x7fffffffffffffffull));
+    uint32_t l = valid ? (uint32_t)p.j : ~0u;
+    const uint64_t mh = h;
+    const uint32_t ml = l;
+    wave_min_key(h, l);
+    const int src = winner_lane(valid && mh == h && ml == l);
+    __shared__ PricePart sw[kBlock / 64];
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        PricePart o{0.0, -1, 0, 0};
+        if (src >= 0) {
+            o.j = (int64_t)l;
+            o.v = __longlong_as_double((long long)rdl64((uint64_t)__double_as_longlong(p.v), src));
+            o.cls = (int32_t)rdl32((uint32_t)p.cls, src);
+        }
+        sw[w] = o;
+    }
+    __syncthreads();
+    PricePart b = sw[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / 64; i++)
+        if (pp_better<RULE>(sw[i], b)) b = sw[i];
+    return b;
+}
+
 // Pricing candidate of column j: dR is the (real)
 // objective row entry; with Big-M (g.nobj == 2) dM is the M-part entry and the
 // comparison is lexicographic (M part first). NaN entries are never eligible.
@@ -372,6 +500,10 @@ __global__ __launch_bounds__(kBlock) void k_prep(double *__restrict__ T, Geo g, 
         }
     }
     const double piv = best.piv;   // == T_t[r][k_t] (select_{t-1} computed and stored it)
+    const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t nvec = (g.ncols + 1) / 2;
+    d2 t = d2{0.0, 0.0};           // the pivot row as stored (issued before the staging barrier)
+    if (own && j2 < nvec) t = *(const d2 *)(T + rl * g.ld + 2 * j2);
     __shared__ double s_c[LPG_DEFER_MAX];
     __shared__ int64_t s_rq[LPG_DEFER_MAX];
     if (DEFER && own) {            // the chain's per-pivot scalars, staged once per block
@@ -382,24 +514,30 @@ __global__ __launch_bounds__(kBlock) void k_prep(double *__restrict__ T, Geo g, 
         __syncthreads();
     }
 
-    const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t nvec = (g.ncols + 1) / 2;
     PricePart pbest{0.0, -1, 0, 0};
     bool live = false;
     if (j2 < nvec) {
         d2 p = d2{0.0, 0.0};
         if (own) {
-            d2 t = *(const d2 *)(T + rl * g.ld + 2 * j2);
             if (DEFER) {   // row r of the current tableau: the pending chain
-#pragma unroll 8
-                for (int q = 0; q < D.q; q++) {
-                    const d2 pq = *(const d2 *)(D.Pbuf + (int64_t)q * g.ld + 2 * j2);
-                    if (s_rq[q] == rl) {
-                        t = pq;
-                    } else {
-                        const double c = s_c[q];
-                        t.x = fma(c, pq.x, t.x);
-                        t.y = fma(c, pq.y, t.y);
+                // chunks of 16 pending rows: all loads of a chunk in flight at once
+                for (int q0 = 0; q0 < D.q; q0 += 16) {
+                    d2 pq[16];
+#pragma unroll
+                    for (int u = 0; u < 16; u++)
+                        if (q0 + u < D.q) pq[u] = *(const d2 *)(D.Pbuf + (int64_t)(q0 + u) * g.ld + 2 * j2);
+#pragma unroll
+                    for (int u = 0; u < 16; u++) {
+                        const int q = q0 + u;
+                        if (q < D.q) {
+                            if (s_rq[q] == rl) {
+                                t = pq[u];
+                            } else {
+                                const double c = s_c[q];
+                                t.x = fma(c, pq[u].x, t.x);
+                                t.y = fma(c, pq[u].y, t.y);
+                            }
+                        }
                     }
                 }
             }
@@ -536,6 +674,14 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
         p0 = P[0];
         pk = P[kn];
     }
+    // this thread's first row: its two tableau loads go out before the staging barrier
+    const int64_t ifirst = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t nrows = g.nloc + g.nobj;
+    double ob0 = 0.0, oa0 = 0.0;
+    if (ifirst < nrows) {
+        ob0 = T[ifirst * g.ld];
+        oa0 = T[ifirst * g.ld + kn];
+    }
     __shared__ double s_p0[LPG_DEFER_MAX + 1], s_pk[LPG_DEFER_MAX + 1];
     __shared__ int64_t s_rq[LPG_DEFER_MAX + 1];
     if (DEFER && !FIRST) {          // the chain's per-pivot scalars, staged once per block
@@ -547,11 +693,10 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
         }
         __syncthreads();
     }
-    const int64_t nrows = g.nloc + g.nobj;
     Cand best{0.0, 0.0, 0, -1};
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * kBlock) {
-        const double ob = T[i * g.ld];
-        const double oa = T[i * g.ld + kn];
+    for (int64_t i = ifirst; i < nrows; i += (int64_t)gridDim.x * kBlock) {
+        const double ob = i == ifirst ? ob0 : T[i * g.ld];
+        const double oa = i == ifirst ? oa0 : T[i * g.ld + kn];
         double b, a;
         if (FIRST) {
             b = ob;
@@ -563,15 +708,24 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
             } else {                    // columns 0 and k_{t+1}: chain over pivots 0..q
                 b = ob;
                 a = oa;
-#pragma unroll 8
-                for (int q = 0; q < D.q; q++) {
-                    const double c = -D.Cbuf[(int64_t)q * D.cs + i];
-                    if (i == s_rq[q]) {
-                        b = s_p0[q];
-                        a = s_pk[q];
-                    } else {
-                        b = fma(c, s_p0[q], b);
-                        a = fma(c, s_pk[q], a);
+                // chunks of 32 pending pivots: all multiplier loads of a chunk in flight at once
+                for (int q0 = 0; q0 < D.q; q0 += 32) {
+                    double cv[32];
+#pragma unroll
+                    for (int u = 0; u < 32; u++)
+                        if (q0 + u < D.q) cv[u] = D.Cbuf[(int64_t)(q0 + u) * D.cs + i];
+#pragma unroll
+                    for (int u = 0; u < 32; u++) {
+                        const int q = q0 + u;
+                        if (q < D.q) {
+                            if (i == s_rq[q]) {
+                                b = s_p0[q];
+                                a = s_pk[q];
+                            } else {
+                                b = fma(-cv[u], s_p0[q], b);
+                                a = fma(-cv[u], s_pk[q], a);
+                            }
+                        }
                     }
                 }
                 if (i == s_rq[D.q]) {       // pivot t itself: C_t is Cs
@@ -625,6 +779,307 @@ int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState 
         else LPG_SEL(RULE_DANTZIG, false, false);
     }
 #undef LPG_SEL
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------
+// Deferred-mode pivot kernels without a communicator (the default path):
+// the same arithmetic as k_prep<FUSE, DEFER> / k_select<DEFER>, with every
+// load that does not depend on this pivot's choices issued at kernel start,
+// so that each kernel has two dependent memory round trips instead of five
+// (prep: [status, candidates, pending P rows, objective rows] -> [pivot row,
+// its multipliers]; select: [status, pricing partials, pending multipliers,
+// column 0] -> [column k, P_q[k]]). At most kPF pending pivots are
+// prefetched; larger blocks load the rest in the chain.
+// ------------------------------------------------------------------------
+
+constexpr int kPF = 32;
+
+#ifdef LPG_PHASES
+// Phase probe (tools/phase_probe.py, built into tools/liblpg_phases.so only):
+// s_memrealtime (100 MHz) stamps of block 0's thread 0 at phase boundaries,
+// plus the earliest start and latest end over all blocks.
+__device__ unsigned long long g_ph[2][16];
+#define LPG_PH(kern, k)                                                                  \
+    do {                                                                                 \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                      \
+        if (threadIdx.x == 0) {                                                          \
+            const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();              \
+            if (blockIdx.x == 0) g_ph[kern][k] = t_;                                     \
+            if ((k) == 0) atomicMin(&g_ph[kern][14], t_);                                \
+            if ((k) == 5) atomicMax(&g_ph[kern][15], t_);                                \
+        }                                                                                \
+    } while (0)
+#else
+#define LPG_PH(kern, k) do { } while (0)
+#endif
+
+template <int RULE>
+__global__ __launch_bounds__(kBlock) void k_prep_d(double *__restrict__ T, Geo g, DevState *st, int s,
+                                                   const Cand *__restrict__ cand, int ncand, double *__restrict__ P,
+                                                   const double *__restrict__ Cs, PricePart *__restrict__ pp, Defer D) {
+    const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t nvec = (g.ncols + 1) / 2;
+    const bool col = j2 < nvec;
+    const int64_t rM = g.nloc, rR = g.nloc + g.nobj - 1;
+    const int lane = threadIdx.x & 63;
+    LPG_PH(0, 0);
+    // ---- round 1: nothing here depends on the leaving row
+    const int32_t status = st->slot[s].status;
+    Cand best{0.0, 0.0, 0, -1};
+    for (int q = threadIdx.x; q < ncand; q += kBlock) {
+        const Cand c = cand[q];
+        if (cand_better(c, best)) best = c;
+    }
+    d2 dM = d2{0.0, 0.0}, dR = d2{0.0, 0.0};
+    if (col) {
+        dM = *(const d2 *)(T + rM * g.ld + 2 * j2);
+        dR = *(const d2 *)(T + rR * g.ld + 2 * j2);
+    }
+    const double cM = -Cs[rM], cR = -Cs[rR];
+    const int npf = D.q < kPF ? D.q : kPF;
+    d2 pq[kPF];
+#pragma unroll
+    for (int u = 0; u < kPF; u++)
+        if (u < npf && col) pq[u] = *(const d2 *)(D.Pbuf + (int64_t)u * g.ld + 2 * j2);
+    const int64_t rqv = lane < D.q ? D.rq[lane] : -1;   // lane q of every wave holds r_q
+    if (status != RUNNING) return;
+    LPG_PH(0, 1);
+    best = block_argmin_cand(best);
+    LPG_PH(0, 2);
+    if (best.row < 0 || !isfinite(best.piv) || !isfinite(best.theta)) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->slot[s].status = best.row < 0 ? UNBOUNDED : NUMERIC;
+            st->slot[s].r = -1;
+        }
+        return;
+    }
+    const int64_t rl = best.row - g.row0;   // single rank: always local
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const int64_t k = st->slot[s].k;
+        st->slot[s].r = best.row;
+        D.rq[D.q] = rl;
+        st->npend = D.q + 1;
+        D.basis[best.row] = k;
+        const int64_t n = st->pivots;
+        if (D.logk && n < st->logcap) {
+            D.logk[n] = k;
+            D.logr[n] = best.row;
+        }
+        st->pivots = n + 1;
+        st->last_k = k;
+        st->last_r = best.row;
+    }
+    // ---- round 2: the pivot row as stored and its pending multipliers
+    // (lane q: -C_q[r]); the chain restarts at the last pending pivot qs on
+    // this row (x = P_qs), found by a ballot, so each step is one fma with
+    // the multiplier read back from lane q (v_readlane: no LDS, no barrier)
+    d2 t = d2{0.0, 0.0};
+    if (col) t = *(const d2 *)(T + rl * g.ld + 2 * j2);
+    const double cl = lane < D.q ? -D.Cbuf[(int64_t)lane * D.cs + rl] : 0.0;
+    const unsigned long long hit = __ballot(lane < D.q && rqv == rl);
+    const int qs = hit ? 63 - __clzll((long long)hit) : -1;
+    LPG_PH(0, 3);
+    PricePart pbest{0.0, -1, 0, 0};
+    const uint64_t clb = (uint64_t)__double_as_longlong(cl);
+    if (col) {
+#pragma unroll
+        for (int u = 0; u < kPF; u++) {
+            if (u < npf) {
+                if (u == qs) {
+                    t = pq[u];
+                } else if (u > qs) {
+                    const double c = __longlong_as_double((long long)rdl64(clb, u));
+                    t.x = fma(c, pq[u].x, t.x);
+                    t.y = fma(c, pq[u].y, t.y);
+                }
+            }
+        }
+        for (int q = kPF; q < D.q; q++) {       // blocks longer than kPF
+            const d2 v = *(const d2 *)(D.Pbuf + (int64_t)q * g.ld + 2 * j2);
+            if (q == qs) {
+                t = v;
+            } else if (q > qs) {
+                const double c = __longlong_as_double((long long)rdl64(clb, q));
+                t.x = fma(c, v.x, t.x);
+                t.y = fma(c, v.y, t.y);
+            }
+        }
+        const double piv = best.piv;
+        d2 p;
+        p.x = t.x / piv;
+        p.y = t.y / piv;
+        *(d2 *)(P + 2 * j2) = p;
+        dM.x = fma(cM, p.x, dM.x);
+        dM.y = fma(cM, p.y, dM.y);
+        dR.x = fma(cR, p.x, dR.x);
+        dR.y = fma(cR, p.y, dR.y);
+        *(d2 *)(T + rR * g.ld + 2 * j2) = dR;
+        if (g.nobj == 2) *(d2 *)(T + rM * g.ld + 2 * j2) = dM;
+        price_one<RULE>(pbest, dM.x, dR.x, 2 * j2, g);
+        price_one<RULE>(pbest, dM.y, dR.y, 2 * j2 + 1, g);
+    }
+    LPG_PH(0, 4);
+    pbest = block_argmin_pp<RULE>(pbest);
+    if (threadIdx.x == 0) pp[blockIdx.x] = pbest;
+    LPG_PH(0, 5);
+}
+
+template <int RULE>
+__global__ __launch_bounds__(kBlock) void k_select_d(const double *__restrict__ T, Geo g, DevState *st, int s,
+                                                     int s1, const double *__restrict__ Cs, double *__restrict__ Cs1,
+                                                     const PricePart *__restrict__ pp, int npp,
+                                                     const int64_t *__restrict__ basis, Cand *__restrict__ part,
+                                                     Defer D) {
+    const int64_t nrows = g.nloc + g.nobj;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;   // one row per thread (launcher checks)
+    const bool row = i < nrows;
+    const bool crow = i < g.nloc;
+    const int lane = threadIdx.x & 63;
+    LPG_PH(1, 0);
+    // ---- round 1: nothing here depends on the entering column
+    const int32_t stt = st->slot[s].status;
+    const int64_t r = st->slot[s].r, kc = st->slot[s].k;
+    PricePart pb{0.0, -1, 0, 0};
+    for (int q = threadIdx.x; q < npp; q += kBlock) {
+        const PricePart c = pp[q];
+        if (pp_better<RULE>(c, pb)) pb = c;
+    }
+    double ob = 0.0, csi = 0.0;
+    if (row) {
+        ob = T[i * g.ld];
+        csi = Cs[i];
+    }
+    const int npf = D.q < kPF ? D.q : kPF;
+    double cv[kPF];
+#pragma unroll
+    for (int u = 0; u < kPF; u++)
+        if (u < npf && crow) cv[u] = D.Cbuf[(int64_t)u * D.cs + i];
+    // lane q of every wave holds P_q[0], r_q (q <= D.q: pivot t included)
+    const bool lq = lane <= D.q;
+    const double p0l = lq ? D.Pbuf[(int64_t)lane * g.ld] : 0.0;
+    const int32_t rql = lq ? (int32_t)D.rq[lane] : -1;
+    const int64_t bkey = (RULE == RULE_BLAND && crow) ? basis[g.row0 + i] : 0;
+    Slot *dst = &st->slot[s1];
+    if (stt != RUNNING) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            dst->status = stt;
+            dst->k = -1;
+            dst->r = -1;
+        }
+        return;
+    }
+    if (crow) D.Cbuf[(int64_t)D.q * D.cs + i] = csi;   // pivot t is pending: its column C_t
+    LPG_PH(1, 1);
+    pb = block_argmin_pp<RULE>(pb);
+    LPG_PH(1, 2);
+    if (pb.j < 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            dst->status = OPTIMAL;
+            dst->k = -1;
+            dst->r = -1;
+        }
+        return;
+    }
+    const int64_t kn = pb.j;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        dst->status = RUNNING;
+        dst->k = kn;
+    }
+    // ---- round 2: column k_{t+1} as stored and P_q[k_{t+1}] (lane q)
+    double oa = 0.0;
+    if (row) oa = T[i * g.ld + kn];
+    const double pkl = lq ? D.Pbuf[(int64_t)lane * g.ld + kn] : 0.0;
+    LPG_PH(1, 3);
+    const uint64_t p0b = (uint64_t)__double_as_longlong(p0l), pkb = (uint64_t)__double_as_longlong(pkl);
+    Cand best{0.0, 0.0, 0, -1};
+    if (row) {
+        double b = ob, a = oa;
+        if (crow) {                   // columns 0 and k_{t+1}: chain over pivots 0..q
+            const int32_t ii = (int32_t)i;
+#pragma unroll
+            for (int u = 0; u < kPF; u++) {
+                if (u < npf) {
+                    const double q0 = __longlong_as_double((long long)rdl64(p0b, u));
+                    const double qk = __longlong_as_double((long long)rdl64(pkb, u));
+                    if (ii == (int32_t)rdl32((uint32_t)rql, u)) {
+                        b = q0;
+                        a = qk;
+                    } else {
+                        b = fma(-cv[u], q0, b);
+                        a = fma(-cv[u], qk, a);
+                    }
+                }
+            }
+            for (int q = kPF; q <= D.q; q++) {   // the rest of a long block, and pivot t itself
+                const double q0 = __longlong_as_double((long long)rdl64(p0b, q));
+                const double qk = __longlong_as_double((long long)rdl64(pkb, q));
+                const double c = q == D.q ? -csi : -D.Cbuf[(int64_t)q * D.cs + i];
+                if (ii == (int32_t)rdl32((uint32_t)rql, q)) {
+                    b = q0;
+                    a = qk;
+                } else {
+                    b = fma(c, q0, b);
+                    a = fma(c, qk, a);
+                }
+            }
+            if (D.q < kPF) {          // pivot t itself: C_t is Cs
+                const int q = D.q;
+                const double q0 = __longlong_as_double((long long)rdl64(p0b, q));
+                const double qk = __longlong_as_double((long long)rdl64(pkb, q));
+                if (ii == (int32_t)rdl32((uint32_t)rql, q)) {
+                    b = q0;
+                    a = qk;
+                } else {
+                    b = fma(-csi, q0, b);
+                    a = fma(-csi, qk, a);
+                }
+            }
+        }                             // objective rows are current (prep wrote d_{t+1})
+        Cs1[i] = a;
+        if (crow && a > g.eps_piv) {
+            const int64_t grow = g.row0 + i;
+            Cand c;
+            c.theta = b > 0.0 ? b / a : 0.0;
+            c.piv = a;
+            c.row = grow;
+            c.key = RULE == RULE_BLAND ? (grow == r ? kc : bkey) : grow;
+            if (cand_better(c, best)) best = c;
+        }
+    }
+    LPG_PH(1, 4);
+    best = block_argmin_cand(best);
+    if (threadIdx.x == 0) part[blockIdx.x] = best;
+    LPG_PH(1, 5);
+}
+
+#ifdef LPG_PHASES
+int debug_phases(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ph), sizeof g_ph) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long init[2][16];
+        for (int k = 0; k < 2; k++)
+            for (int j = 0; j < 16; j++) init[k][j] = j == 14 ? ~0ull : 0ull;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_ph), init, sizeof init) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
+int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, Cand *part, int nsel,
+                   double *P, const double *Cs, double *Cs1, PricePart *pp, int npp, const int64_t *basis,
+                   const Defer &D) {
+    if ((int64_t)nsel * kBlock < g.nloc + g.nobj) return -1;   // k_select_d: one row per thread
+    hipStream_t stream = (hipStream_t)L.stream;
+    if (rule == RULE_BLAND) {
+        hipLaunchKernelGGL(k_prep_d<RULE_BLAND>, dim3(npp), dim3(kBlock), 0, stream, g.T, g, st, s, part, nsel, P, Cs, pp, D);
+        hipLaunchKernelGGL(k_select_d<RULE_BLAND>, dim3(nsel), dim3(kBlock), 0, stream, g.T, g, st, s, s1, Cs, Cs1, pp,
+                           npp, basis, part, D);
+    } else {
+        hipLaunchKernelGGL(k_prep_d<RULE_DANTZIG>, dim3(npp), dim3(kBlock), 0, stream, g.T, g, st, s, part, nsel, P, Cs, pp, D);
+        hipLaunchKernelGGL(k_select_d<RULE_DANTZIG>, dim3(nsel), dim3(kBlock), 0, stream, g.T, g, st, s, s1, Cs, Cs1, pp,
+                           npp, basis, part, D);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1216,8 +1671,8 @@ __global__ __launch_bounds__(kBlock) void k_flush(double *__restrict__ T, Geo g,
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-template <int KMAX, int NPAIR, bool NT, int SR>
-__global__ __launch_bounds__(kBlock) void k_flushm(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+template <int KMAX, int NPAIR, bool NT, int SR, int LB>
+__global__ __launch_bounds__(kBlock, LB > 0 ? LB : 1) void k_flushm(double *__restrict__ T, Geo g, DevState *__restrict__ st,
                                                    const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
                                                    int64_t cs, int64_t ntiles, int64_t nitems, int skip) {
     constexpr int G = KMAX / 4;             // MFMA k-steps
@@ -1302,18 +1757,27 @@ __global__ __launch_bounds__(kBlock) void k_flushm(double *__restrict__ T, Geo g
             const bool more = i + 16 < i1;
             d2 tn[NPAIR][4];
             if (more) load(tn, i + 16);
-            double a[G];
             const int lr = (int)(i - i0) + lc;
-#pragma unroll
-            for (int gq = 0; gq < G; gq++) a[gq] = -sC[(4 * gq + lk) * SR + lr];
 #pragma unroll
             for (int pp = 0; pp < NPAIR; pp++) {
                 d4 ae = d4{t[pp][0].x, t[pp][1].x, t[pp][2].x, t[pp][3].x};
                 d4 ao = d4{t[pp][0].y, t[pp][1].y, t[pp][2].y, t[pp][3].y};
+                // A fragments from LDS in groups of 4 k-steps (a compiler fence between
+                // groups keeps at most 8 of them live: fewer VGPRs, more waves per SIMD)
 #pragma unroll
-                for (int gq = 0; gq < G; gq++) {
-                    ae = __builtin_amdgcn_mfma_f64_16x16x4f64(a[gq], b[pp][0][gq], ae, 0, 0, 0);
-                    ao = __builtin_amdgcn_mfma_f64_16x16x4f64(a[gq], b[pp][1][gq], ao, 0, 0, 0);
+                for (int g0 = 0; g0 < G; g0 += 4) {
+                    double a[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (g0 + u < G) a[u] = -sC[(4 * (g0 + u) + lk) * SR + lr];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (g0 + u < G) {
+                            ae = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[pp][0][g0 + u], ae, 0, 0, 0);
+                            ao = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[pp][1][g0 + u], ao, 0, 0, 0);
+                        }
+                    }
+                    if (LB > 0) asm volatile("" ::: "memory");
                 }
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
@@ -1332,6 +1796,99 @@ __global__ __launch_bounds__(kBlock) void k_flushm(double *__restrict__ T, Geo g
             for (int pp = 0; pp < NPAIR; pp++)
 #pragma unroll
                 for (int r = 0; r < 4; r++) t[pp][r] = tn[pp][r];
+        }
+    }
+    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
+}
+
+// k_flushs: the matrix-core flush with ONE column per lane (16 columns per
+// wave, 8-byte accesses, one 16x16 MFMA tile per 16-row step). Half the B
+// fragments of k_flushm per lane, so 64-pivot blocks keep 4+ waves per SIMD.
+// DYN: dynamic dequeue of items; otherwise a static grid stride.
+template <int KMAX, bool NT, int SR, bool DYN>
+__global__ __launch_bounds__(kBlock) void k_flushs(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                   const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
+                                                   int64_t cs, int64_t ntiles, int64_t nitems, int skip) {
+    constexpr int G = KMAX / 4;
+    __shared__ __attribute__((aligned(16))) double sC[KMAX * SR];
+    const int np = (int)st->npend;
+    if (np <= 0) return;
+    const int64_t ld = g.ld;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lc = lane & 15, lk = lane >> 4;
+    unsigned long long touched = 0;
+    __shared__ int64_t next_item;
+    for (int64_t item = DYN ? -1 : blockIdx.x;; item += DYN ? 0 : gridDim.x) {
+        if (DYN) {
+            __syncthreads();
+            if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
+            __syncthreads();
+            item = next_item;
+        } else {
+            __syncthreads();   // sC of the previous item is no longer read
+        }
+        if (item >= nitems) break;
+        const int64_t tile = item % ntiles, strip = item / ntiles;
+        const int64_t i0 = strip * SR;
+        const int64_t i1 = i0 + SR < g.nloc ? i0 + SR : g.nloc;
+        const int64_t col = tile * 64 + wave * 16 + lc;
+        const bool in = col < g.ncols;
+        double b[G];
+        bool live = false;
+#pragma unroll
+        for (int gq = 0; gq < G; gq++) {
+            const int q = 4 * gq + lk;
+            b[gq] = (in && q < np) ? Pbuf[(int64_t)q * ld + col] : 0.0;
+            live = live || b[gq] != 0.0;
+        }
+        live = (__shfl_xor((int)live, 16, 64) | (int)live) != 0;
+        live = (__shfl_xor((int)live, 32, 64) | (int)live) != 0;
+        const bool ok = in && (!skip || live);
+        const int cnt = __syncthreads_count(ok);    // 4 lanes per column
+        if (cnt == 0) continue;
+        if (threadIdx.x == 0) touched += (unsigned long long)(cnt / 4) * (unsigned long long)(i1 - i0);
+        for (int e = threadIdx.x; e < KMAX * SR / 2; e += kBlock) {
+            const int q = e / (SR / 2), rr = 2 * (e % (SR / 2));
+            d2 v = d2{0.0, 0.0};
+            if (q < np && i0 + rr < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + i0 + rr);   // i0 + rr + 1 < cs
+            *(d2 *)(sC + q * SR + rr) = v;
+        }
+        __syncthreads();
+        double *cp = T + col;
+        d4 t;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int64_t row = i0 + lk + 4 * r;
+            const double *a = cp + row * ld;
+            t[r] = (ok && row < i1) ? (NT ? __builtin_nontemporal_load(a) : *a) : 0.0;
+        }
+        for (int64_t i = i0;;) {
+            const bool more = i + 16 < i1;
+            d4 tn;
+            if (more) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = i + 16 + lk + 4 * r;
+                    const double *a = cp + row * ld;
+                    tn[r] = (ok && row < i1) ? (NT ? __builtin_nontemporal_load(a) : *a) : 0.0;
+                }
+            }
+            const int lr = (int)(i - i0) + lc;
+#pragma unroll
+            for (int gq = 0; gq < G; gq++)
+                t = __builtin_amdgcn_mfma_f64_16x16x4f64(-sC[(4 * gq + lk) * SR + lr], b[gq], t, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int64_t row = i + lk + 4 * r;
+                if (ok && row < i1) {
+                    double *d = cp + row * ld;
+                    if (NT) __builtin_nontemporal_store(t[r], d);
+                    else *d = t[r];
+                }
+            }
+            if (!more) break;
+            i += 16;
+            t = tn;
         }
     }
     if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
@@ -1384,6 +1941,13 @@ static const FlushCfg kFlushCfgs[] = {
     {1, 1, true, true, 64, 8},      // 11
     {1, 1, true, true, 32, 8},      // 12
     {1, 1, true, true, 32, 4},      // 13
+    {2, 1, true, true, 64, 4},      // 14 MFMA, one column per lane, dynamic dequeue
+    {2, 0, true, true, 64, 4},      // 15 same, static grid stride
+    {2, 1, true, true, 128, 2},     // 16 128-row strips
+    {2, 1, false, true, 64, 4},     // 17 temporal loads / stores
+    {2, 0, true, true, 64, 8},      // 18 static, 8 blocks per CU
+    {1, 1, true, true, 128, 104},   // 19 = 8 with __launch_bounds__(256, 3) and grouped A fragments
+    {1, 1, true, true, 64, 104},    // 20 same, 64-row strips
 };
 constexpr int kNumFlushCfgs = sizeof(kFlushCfgs) / sizeof(kFlushCfgs[0]);
 constexpr int kDefaultFlushCfg = 8;
@@ -1406,23 +1970,60 @@ int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, in
     FlushCfg cfg = kFlushCfgs[variant];
     hipStream_t stream = (hipStream_t)L.stream;
     const int64_t ntiles_p = (g.ncols + kBlock - 1) / kBlock;   // k_flush_pivot_rows column tiles
-    if (cfg.mfma) {
+    if (cfg.mfma == 2) {                                     // k_flushs: ru = DYN
+        const int64_t ntiles = (g.ncols + 63) / 64;
+        int strip = cfg.strip;
+        while (strip > 32 && ntiles * ((g.nloc + strip - 1) / strip) < 4096) strip /= 2;
+        while (strip > 32 && kmax * strip * 8 > 65536) strip /= 2;   // LDS tile of C <= 64 KB
+        const int64_t nitems = ntiles * ((g.nloc + strip - 1) / strip);
+        const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * cfg.per_cu);
+        if (nblocks < 1) return 0;
+#define LPG_FS(K, N, S, DY)                                                                                          \
+    hipLaunchKernelGGL((k_flushs<K, N, S, DY>), dim3((unsigned)nblocks), dim3(kBlock), 0, stream, g.T, g, st, D.Pbuf, \
+                       D.Cbuf, D.cs, ntiles, nitems, skip)
+#define LPG_FS_S(K, N, DY)                       \
+    switch (strip) {                             \
+        case 32: LPG_FS(K, N, 32, DY); break;    \
+        case 64: LPG_FS(K, N, 64, DY); break;    \
+        default: LPG_FS(K, N, 128, DY); break;   \
+    }
+#define LPG_FS_K(N, DY)                          \
+    switch (kmax) {                              \
+        case 8: LPG_FS_S(8, N, DY); break;       \
+        case 16: LPG_FS_S(16, N, DY); break;     \
+        case 32: LPG_FS_S(32, N, DY); break;     \
+        default: LPG_FS_S(64, N, DY); break;     \
+    }
+        if (cfg.nt) { if (cfg.ru) LPG_FS_K(true, true) else LPG_FS_K(true, false) }
+        else { if (cfg.ru) LPG_FS_K(false, true) else LPG_FS_K(false, false) }
+#undef LPG_FS_K
+#undef LPG_FS_S
+#undef LPG_FS
+    } else if (cfg.mfma) {
         const int64_t bcols = 4 * 32 * cfg.ru;
         const int64_t ntiles = (g.ncols + bcols - 1) / bcols;
         int strip = cfg.strip;
         while (strip > 32 && ntiles * ((g.nloc + strip - 1) / strip) < 4096) strip /= 2;
         while (strip > 32 && kmax * strip * 8 > 32768) strip /= 2;   // LDS tile of C <= 32 KB
         const int64_t nitems = ntiles * ((g.nloc + strip - 1) / strip);
-        const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * cfg.per_cu);
+        const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * (cfg.per_cu % 100));
         if (nblocks < 1) return 0;
 #define LPG_FM(K, NP, N, S)                                                                                          \
-    hipLaunchKernelGGL((k_flushm<K, NP, N, S>), dim3((unsigned)nblocks), dim3(kBlock), 0, stream, g.T, g, st, D.Pbuf, \
-                       D.Cbuf, D.cs, ntiles, nitems, skip)
-#define LPG_FM_S(K, NP, N)                                              \
-    switch (strip) {                                                    \
-        case 32: LPG_FM(K, NP, N, 32); break;                           \
-        case 64: LPG_FM(K, NP, N, 64); break;                           \
-        default: LPG_FM(K, NP, N, 128); break;                          \
+    do {                                                                                                             \
+        if (cfg.per_cu >= 100)                                                                                       \
+            hipLaunchKernelGGL((k_flushm<K, NP, N, S, (NP == 1 ? 3 : 0)>), dim3((unsigned)nblocks), dim3(kBlock), 0,   \
+                               stream, g.T, g, st, D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, skip);                       \
+        else                                                                                                         \
+            hipLaunchKernelGGL((k_flushm<K, NP, N, S, 0>), dim3((unsigned)nblocks), dim3(kBlock), 0, stream, g.T, g,  \
+                               st, D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, skip);                                       \
+    } while (0)
+// strips are capped so that the C tile stays <= 32 KB (the launcher guarantees it; the
+// expressions keep larger tiles from being instantiated at all)
+#define LPG_FM_S(K, NP, N)                                                              \
+    switch (strip) {                                                                    \
+        case 32: LPG_FM(K, NP, N, 32); break;                                           \
+        case 64: LPG_FM(K, NP, N, (K * 64 * 8 <= 32768 ? 64 : 32)); break;              \
+        default: LPG_FM(K, NP, N, (K * 128 * 8 <= 32768 ? 128 : 64)); break;            \
     }
 #define LPG_FM_K(NP, N)                         \
     switch (kmax) {                             \

@@ -104,7 +104,7 @@ def test_enqueue_past_optimal_partial_block(lpg, monkeypatch):
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("variant", list(range(14)))
+@pytest.mark.parametrize("variant", list(range(21)))
 def test_flush_variants_identical(lpg, monkeypatch, variant):
     monkeypatch.setenv("LPG_FLUSH_VARIANT", str(variant))
     m, n = 300, 700
@@ -150,7 +150,7 @@ def test_bad_block_size(lpg, monkeypatch):
         lpg.Engine(8, 20)
 
 
-@pytest.mark.parametrize("variant", [7, 8, 9])
+@pytest.mark.parametrize("variant", [7, 8, 9, 14, 15, 19])
 @pytest.mark.parametrize("k", [3, 8, 32, 64])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1)])
 def test_flush_kernels_block_sizes(lpg, monkeypatch, variant, k, m, n, seed, kind, rule):
@@ -165,3 +165,22 @@ def test_flush_kernels_block_sizes(lpg, monkeypatch, variant, k, m, n, seed, kin
     ores = o.solve(200_000, rule)
     assert res.status == ores.status == 1 and res.pivots == ores.pivots
     _assert_same(e, o, m)
+
+
+@pytest.mark.parametrize("k", [5, 32])
+@pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1)])
+def test_generic_and_prefetching_pivot_kernels_agree(lpg, monkeypatch, k, m, n, seed, kind, rule):
+    """The deferred single-rank pivot runs through k_prep_d / k_select_d; the generic
+    k_prep / k_select pair (LPG_SLOW_PIVOT=1, also the multi-rank path) must give the
+    same bits."""
+    monkeypatch.setenv("LPG_SLOW_PIVOT", "1")
+    f = _engine(lpg, monkeypatch, k, m, n + m + 1)
+    monkeypatch.delenv("LPG_SLOW_PIVOT")
+    e = _engine(lpg, monkeypatch, k, m, n + m + 1)
+    o = Oracle(m, n + m + 1)
+    for x in (e, f, o):
+        x.generate(n, seed, kind)
+    res, fres, ores = e.solve(200_000, rule), f.solve(200_000, rule), o.solve(200_000, rule)
+    assert res.pivots == fres.pivots == ores.pivots
+    _assert_same(e, o, m)
+    _assert_same(f, o, m)
