@@ -10,6 +10,6 @@ rc=$?; echo "pytest rc=$rc" >&2; [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python bench.py > gpurun_out/bench_config3.json 2> gpurun_out/bench.err || exit $?
 timeout -k 10 200 python bench.py --config 2 --steps 1500 --no-cpu > gpurun_out/bench_config2.json 2>> gpurun_out/bench.err || exit $?
 timeout -k 10 300 python bench.py --config 5 > gpurun_out/bench_config5.json 2>> gpurun_out/bench.err || exit $?
-timeout -k 10 300 python bench.py --config 4 --steps 20 --warmup 2 --no-cpu > gpurun_out/bench_config4.json 2>> gpurun_out/bench.err || exit $?
+timeout -k 10 400 python bench.py --config 4 --steps 64 --warmup 2 --no-cpu > gpurun_out/bench_config4.json 2>> gpurun_out/bench.err || exit $?
 if [ -z "${NO_PROFILE:-}" ]; then ./tools/profile.sh || exit $?; fi
 exit $rc

@@ -8,15 +8,15 @@ set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 CFG=${CFG:-3}
-STEPS=${STEPS:-50}
+STEPS=${STEPS:-64}   # whole deferred blocks (2 x 32), no warm-up: every k_flushm launch applies 32 pivots
 mkdir -p $OUT
 echo "[profile] trace" >&2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    python3 bench.py --config $CFG --steps $STEPS --warmup 3 --no-cpu > $OUT/trace_bench.json 2> $OUT/trace.err || exit $?
+    python3 bench.py --config $CFG --steps $STEPS --warmup 0 --no-cpu > $OUT/trace_bench.json 2> $OUT/trace.err || exit $?
 echo "[profile] fetch" >&2
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
-    python3 bench.py --config $CFG --steps 10 --warmup 2 --no-cpu > $OUT/fetch_bench.json 2> $OUT/fetch.err || exit $?
+    python3 bench.py --config $CFG --steps $STEPS --warmup 0 --no-cpu > $OUT/fetch_bench.json 2> $OUT/fetch.err || exit $?
 echo "[profile] write" >&2
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
-    python3 bench.py --config $CFG --steps 10 --warmup 2 --no-cpu > $OUT/write_bench.json 2> $OUT/write.err || exit $?
+    python3 bench.py --config $CFG --steps $STEPS --warmup 0 --no-cpu > $OUT/write_bench.json 2> $OUT/write.err || exit $?
 find $OUT -name "*.csv" | head -50 >&2
