@@ -289,7 +289,8 @@ static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
 }
 
 static constexpr int kGraphPivots = 32;
-static constexpr int kDefaultDefer = 32;   // pivots per flush (LPG_DEFER)
+static constexpr int kDefaultDefer = 64;        // pivots per flush (LPG_DEFER), large tableaus
+static constexpr int kDefaultDeferSmall = 32;   // tableaus below 512 MB per rank
 
 static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule);
 
@@ -522,7 +523,12 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     const char *ns = getenv("LPG_NO_SKIP");
     c->skip = ((flags & LPG_FLAG_NO_SKIP) || (ns && atoi(ns))) ? 0 : 1;
     const char *dk = getenv("LPG_DEFER");
-    c->defer_k = (flags & LPG_FLAG_EAGER) ? 0 : (dk ? atoi(dk) : kDefaultDefer);
+    // default block: 64 pivots once this rank's tableau is >= 512 MB (the
+    // flush dominates; k_flushw keeps 64-pivot flushes memory-bound), 32 below
+    // (the per-pivot chains dominate: config 2 runs 66k pivots/s at 32, 59k at 64)
+    const int64_t nloc_guess = m * (rank + 1) / world - m * rank / world;
+    const int kdef = (double)nloc_guess * (double)ncols * 8.0 >= 512e6 ? kDefaultDefer : kDefaultDeferSmall;
+    c->defer_k = (flags & LPG_FLAG_EAGER) ? 0 : (dk ? atoi(dk) : kdef);
     if (c->defer_k < 0 || c->defer_k > LPG_DEFER_MAX || (c->defer_k && !flush_kmax_supported(c->defer_k))) {
         fail(c, LPG_ERR_ARG, "LPG_DEFER=%d out of range [0, %d]", c->defer_k, LPG_DEFER_MAX);
         snprintf(g_err, sizeof g_err, "%s", c->err);

@@ -790,10 +790,10 @@ int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState 
 // (prep: [status, candidates, pending P rows, objective rows] -> [pivot row,
 // its multipliers]; select: [status, pricing partials, pending multipliers,
 // column 0] -> [column k, P_q[k]]). At most kPF pending pivots are
-// prefetched; larger blocks load the rest in the chain.
+// prefetched (kPF = 32 for the first half of a block, 64 after; one block
+// per CU at most, so the registers are there); longer chains would load the
+// rest in the chain.
 // ------------------------------------------------------------------------
-
-constexpr int kPF = 32;
 
 #ifdef LPG_PHASES
 // Phase probe (tools/phase_probe.py, built into tools/liblpg_phases.so only):
@@ -814,7 +814,7 @@ __device__ unsigned long long g_ph[2][16];
 #define LPG_PH(kern, k) do { } while (0)
 #endif
 
-template <int RULE>
+template <int RULE, int kPF>
 __global__ __launch_bounds__(kBlock) void k_prep_d(double *__restrict__ T, Geo g, DevState *st, int s,
                                                    const Cand *__restrict__ cand, int ncand, double *__restrict__ P,
                                                    const double *__restrict__ Cs, PricePart *__restrict__ pp, Defer D) {
@@ -925,7 +925,7 @@ __global__ __launch_bounds__(kBlock) void k_prep_d(double *__restrict__ T, Geo g
     LPG_PH(0, 5);
 }
 
-template <int RULE>
+template <int RULE, int kPF>
 __global__ __launch_bounds__(kBlock) void k_select_d(const double *__restrict__ T, Geo g, DevState *st, int s,
                                                      int s1, const double *__restrict__ Cs, double *__restrict__ Cs1,
                                                      const PricePart *__restrict__ pp, int npp,
@@ -1071,15 +1071,22 @@ int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s,
                    const Defer &D) {
     if ((int64_t)nsel * kBlock < g.nloc + g.nobj) return -1;   // k_select_d: one row per thread
     hipStream_t stream = (hipStream_t)L.stream;
+#define LPG_PD(R, PF)                                                                                             \
+    do {                                                                                                          \
+        hipLaunchKernelGGL((k_prep_d<R, PF>), dim3(npp), dim3(kBlock), 0, stream, g.T, g, st, s, part, nsel, P, Cs, \
+                           pp, D);                                                                                \
+        hipLaunchKernelGGL((k_select_d<R, PF>), dim3(nsel), dim3(kBlock), 0, stream, g.T, g, st, s, s1, Cs, Cs1,   \
+                           pp, npp, basis, part, D);                                                              \
+    } while (0)
+    const bool wide = D.q >= 32;            // pending chain longer than 32: the 64-slot prefetch forms
     if (rule == RULE_BLAND) {
-        hipLaunchKernelGGL(k_prep_d<RULE_BLAND>, dim3(npp), dim3(kBlock), 0, stream, g.T, g, st, s, part, nsel, P, Cs, pp, D);
-        hipLaunchKernelGGL(k_select_d<RULE_BLAND>, dim3(nsel), dim3(kBlock), 0, stream, g.T, g, st, s, s1, Cs, Cs1, pp,
-                           npp, basis, part, D);
+        if (wide) LPG_PD(RULE_BLAND, 64);
+        else LPG_PD(RULE_BLAND, 32);
     } else {
-        hipLaunchKernelGGL(k_prep_d<RULE_DANTZIG>, dim3(npp), dim3(kBlock), 0, stream, g.T, g, st, s, part, nsel, P, Cs, pp, D);
-        hipLaunchKernelGGL(k_select_d<RULE_DANTZIG>, dim3(nsel), dim3(kBlock), 0, stream, g.T, g, st, s, s1, Cs, Cs1, pp,
-                           npp, basis, part, D);
+        if (wide) LPG_PD(RULE_DANTZIG, 64);
+        else LPG_PD(RULE_DANTZIG, 32);
     }
+#undef LPG_PD
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1894,6 +1901,133 @@ __global__ __launch_bounds__(kBlock) void k_flushs(double *__restrict__ T, Geo g
     if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
 }
 
+// k_flushw: k_flushm's wave tile (16 rows x 32 columns, 16-byte accesses,
+// even/odd-column MFMA chains, B fragments in VGPRs) on TALL items, which is
+// what keeps 64-pivot blocks memory-bound. A block's 4 waves sweep `rows`
+// rows (runtime, multiple of 16) of a 128-column tile in 16-row bands, in
+// step: the multipliers of band s (-C_q[i] in A-fragment order [q][row],
+// 8 KB at KMAX = 64) sit in an NB-deep LDS ring, loaded into registers one
+// band ahead and written one barrier later, and tableau band s+1 is loaded
+// while band s is on the matrix cores. k_flushm instead stages the C of a
+// whole 64-128-row strip per item (the LDS tile caps the strip at 64 rows
+// for 64 slots) and restarts its pipeline per item: 2.36 ms vs 1.64 ms for
+// this kernel at config 3, K = 64 (tools/flush_lab.hip,
+// profiles/r01_flush_lab_k64.log). Same chain, same MFMA, bitwise identical.
+template <int KMAX, int NB, int LB>
+__global__ __launch_bounds__(kBlock, LB) void k_flushw(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                       const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
+                                                       int64_t cs, int64_t ntiles, int64_t nitems, int64_t rows,
+                                                       int skip) {
+    constexpr int G = KMAX / 4;
+    constexpr int BAND = KMAX * 16;                 // doubles per band
+    constexpr int PER = BAND / 2 / kBlock;          // 16-byte multiplier pieces per thread per band
+    static_assert(PER >= 1 && BAND / 2 % kBlock == 0, "band staging");
+    __shared__ __attribute__((aligned(16))) double sC[NB][BAND];
+    __shared__ int64_t next_item;
+    __shared__ int wsum[kBlock / 64];
+    const int np = (int)st->npend;
+    if (np <= 0) return;
+    const int64_t ld = g.ld;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lc = lane & 15, lk = lane >> 4;
+    unsigned long long touched = 0;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
+        __syncthreads();
+        const int64_t item = next_item;
+        if (item >= nitems) break;
+        const int64_t tile = item % ntiles, strip = item / ntiles;
+        const int64_t i0 = strip * rows;
+        const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
+        const int64_t cl = tile * 128 + wave * 32 + 2 * lc;   // this lane's column pair
+        const bool in = cl < g.ncols;                         // cl even, ld even: cl + 1 < ld
+        double be[G], bo[G];
+        bool live = false;
+#pragma unroll
+        for (int gq = 0; gq < G; gq++) {
+            const int q = 4 * gq + lk;
+            d2 v = d2{0.0, 0.0};
+            if (in && q < np) v = *(const d2 *)(Pbuf + (int64_t)q * ld + cl);
+            be[gq] = v.x;
+            bo[gq] = v.y;
+            live = live || v.x != 0.0 || v.y != 0.0;
+        }
+        // a column pair is live if any of its P entries over all slots is
+        // non-zero: OR over the 4 lanes holding its k-slices
+        live = (__shfl_xor((int)live, 16, 64) | (int)live) != 0;
+        live = (__shfl_xor((int)live, 32, 64) | (int)live) != 0;
+        const bool ok = in && (!skip || live);
+        int mine = (lk == 0 && ok) ? (cl + 1 < g.ncols ? 2 : 1) : 0;   // live doubles per row, pairs counted once
+        for (int mask = 32; mask > 0; mask >>= 1) mine += __shfl_xor(mine, mask, 64);
+        const bool wlive = mine > 0;                                   // wave-uniform
+        if (lane == 0) wsum[wave] = mine;
+        if (__syncthreads_count(wlive && lane == 0) == 0) continue;    // the whole tile is skipped
+        if (threadIdx.x == 0)
+            touched += (unsigned long long)(wsum[0] + wsum[1] + wsum[2] + wsum[3]) * (unsigned long long)(i1 - i0);
+        const int nb = (int)((i1 - i0 + 15) / 16);
+        // multiplier piece e of band s: slot q = e / 8, band rows 2 (e % 8) .. +1
+        // (zeros past np and past i1: A = -0 there, x + -0 == x)
+        auto cload = [&](d2 (&cr)[PER], int s) {
+#pragma unroll
+            for (int u = 0; u < PER; u++) {
+                const int e = threadIdx.x + u * kBlock;
+                const int q = e >> 3, rr = 2 * (e & 7);
+                const int64_t row = i0 + 16 * s + rr;
+                d2 v = d2{0.0, 0.0};
+                if (s < nb && q < np && row < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + row);   // row + 1 < cs
+                cr[u] = -v;
+            }
+        };
+        auto cstore = [&](const d2 (&cr)[PER], int s) {
+#pragma unroll
+            for (int u = 0; u < PER; u++) *(d2 *)(&sC[s % NB][2 * (threadIdx.x + u * kBlock)]) = cr[u];
+        };
+        for (int s = 0; s < NB - 1; s++) {   // prologue: bands 0 .. NB-2 into the ring
+            d2 cr[PER];
+            cload(cr, s);
+            cstore(cr, s);
+        }
+        d2 cn[PER];
+        cload(cn, NB - 1);
+        auto tload = [&](d2 (&x)[4], int s) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int64_t row = i0 + 16 * s + lk + 4 * r;
+                x[r] = (ok && row < i1) ? __builtin_nontemporal_load((const d2 *)(T + row * ld + cl)) : d2{0.0, 0.0};
+            }
+        };
+        d2 t[4];
+        tload(t, 0);
+        for (int s = 0; s < nb; s++) {
+            d2 tn[4];
+            if (s + 1 < nb) tload(tn, s + 1);
+            __syncthreads();                  // band s is staged; ring slot (s - 1) % NB is free
+            cstore(cn, s + NB - 1);
+            cload(cn, s + NB);
+            if (wlive) {
+                d4 ae = d4{t[0].x, t[1].x, t[2].x, t[3].x};
+                d4 ao = d4{t[0].y, t[1].y, t[2].y, t[3].y};
+                const double *sa = &sC[s % NB][lk * 16 + lc];
+#pragma unroll
+                for (int gq = 0; gq < G; gq++) {
+                    const double a = sa[gq * 64];
+                    ae = __builtin_amdgcn_mfma_f64_16x16x4f64(a, be[gq], ae, 0, 0, 0);
+                    ao = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bo[gq], ao, 0, 0, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = i0 + 16 * s + lk + 4 * r;
+                    if (ok && row < i1) __builtin_nontemporal_store(d2{ae[r], ao[r]}, (d2 *)(T + row * ld + cl));
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) t[r] = tn[r];
+        }
+    }
+    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
+}
+
 // The pivot rows of the block, after k_flush: row r_q (last occurrence q in
 // the block) = P_q, continued by the chain of the later pivots. These values
 // do not depend on T_base, so the rows k_flush wrote without the replacement
@@ -1948,9 +2082,14 @@ static const FlushCfg kFlushCfgs[] = {
     {2, 0, true, true, 64, 8},      // 18 static, 8 blocks per CU
     {1, 1, true, true, 128, 104},   // 19 = 8 with __launch_bounds__(256, 3) and grouped A fragments
     {1, 1, true, true, 64, 104},    // 20 same, 64-row strips
+    {3, 2, true, true, 512, 0},     // 21 k_flushw: 512-row items, 2-deep C ring (blocks/CU: 2 at 64 slots, else 3)
+    {3, 3, true, true, 512, 0},     // 22 same, 3-deep ring
+    {3, 2, true, true, 256, 0},     // 23 256-row items
+    {3, 2, true, true, 1024, 0},    // 24 1024-row items
 };
 constexpr int kNumFlushCfgs = sizeof(kFlushCfgs) / sizeof(kFlushCfgs[0]);
-constexpr int kDefaultFlushCfg = 8;
+constexpr int kDefaultFlushCfg = 8;       // blocks of <= 32 pivots: k_flushm
+constexpr int kDefaultFlushCfg64 = 21;    // 64-pivot blocks: k_flushw
 
 int flush_kmax_supported(int k) {
     if (k <= 8) return 8;
@@ -1966,11 +2105,31 @@ static_assert(offsetof(DevState, fwork) == offsetof(DevState, npend) + sizeof(in
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant) {
     kmax = flush_kmax_supported(kmax);
     if (!kmax) return -1;
-    if (variant < 0 || variant >= kNumFlushCfgs) variant = kDefaultFlushCfg;
+    if (variant < 0 || variant >= kNumFlushCfgs) variant = kmax == 64 ? kDefaultFlushCfg64 : kDefaultFlushCfg;
     FlushCfg cfg = kFlushCfgs[variant];
     hipStream_t stream = (hipStream_t)L.stream;
     const int64_t ntiles_p = (g.ncols + kBlock - 1) / kBlock;   // k_flush_pivot_rows column tiles
-    if (cfg.mfma == 2) {                                     // k_flushs: ru = DYN
+    if (cfg.mfma == 3) {                                     // k_flushw: ru = ring depth, strip = rows per item
+        const int64_t ntiles = (g.ncols + 127) / 128;
+        int64_t rows = cfg.strip;
+        while (rows > 64 && ntiles * ((g.nloc + rows - 1) / rows) < 2048) rows /= 2;   // small tableaus: fill the chip
+        const int64_t nitems = ntiles * ((g.nloc + rows - 1) / rows);
+        const int lb = kmax == 64 ? 2 : 3;                   // VGPRs: 184 at 64 slots, <= 128 below (8-32: the 32 form)
+        const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * lb);
+        if (nblocks < 1) return 0;
+#define LPG_FW(K, NB, LBV)                                                                                            \
+    hipLaunchKernelGGL((k_flushw<K, NB, LBV>), dim3((unsigned)nblocks), dim3(kBlock), 0, stream, g.T, g, st, D.Pbuf, \
+                       D.Cbuf, D.cs, ntiles, nitems, rows, skip)
+#define LPG_FW_K(NB)                                  \
+    switch (kmax) {                                   \
+        case 64: LPG_FW(64, NB, 2); break;            \
+        default: LPG_FW(32, NB, 3); break;            \
+    }
+        if (cfg.ru == 3) { LPG_FW_K(3) }
+        else { LPG_FW_K(2) }
+#undef LPG_FW_K
+#undef LPG_FW
+    } else if (cfg.mfma == 2) {                                     // k_flushs: ru = DYN
         const int64_t ntiles = (g.ncols + 63) / 64;
         int strip = cfg.strip;
         while (strip > 32 && ntiles * ((g.nloc + strip - 1) / strip) < 4096) strip /= 2;

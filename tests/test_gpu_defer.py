@@ -104,11 +104,12 @@ def test_enqueue_past_optimal_partial_block(lpg, monkeypatch):
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("variant", list(range(21)))
-def test_flush_variants_identical(lpg, monkeypatch, variant):
+@pytest.mark.parametrize("k", [32, 64])
+@pytest.mark.parametrize("variant", list(range(25)))
+def test_flush_variants_identical(lpg, monkeypatch, variant, k):
     monkeypatch.setenv("LPG_FLUSH_VARIANT", str(variant))
     m, n = 300, 700
-    e = _engine(lpg, monkeypatch, 32, m, n + m + 1)
+    e = _engine(lpg, monkeypatch, k, m, n + m + 1)
     o = Oracle(m, n + m + 1)
     e.generate(n, 24, 0)
     o.generate(n, 24, 0)
@@ -150,12 +151,13 @@ def test_bad_block_size(lpg, monkeypatch):
         lpg.Engine(8, 20)
 
 
-@pytest.mark.parametrize("variant", [7, 8, 9, 14, 15, 19])
+@pytest.mark.parametrize("variant", [7, 8, 9, 14, 15, 19, 21, 22, 23])
 @pytest.mark.parametrize("k", [3, 8, 32, 64])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1)])
 def test_flush_kernels_block_sizes(lpg, monkeypatch, variant, k, m, n, seed, kind, rule):
-    """VALU (7) and matrix-core (8, 9) flushes at every compiled block bound, to
-    optimality, against the oracle (odd shapes: ragged column tiles and strips)."""
+    """VALU (7), matrix-core (8, 9, 14, 15, 19) and tall-item banded (21-23)
+    flushes at every compiled block bound, to optimality, against the oracle
+    (odd shapes: ragged column tiles, strips and bands)."""
     monkeypatch.setenv("LPG_FLUSH_VARIANT", str(variant))
     e = _engine(lpg, monkeypatch, k, m, n + m + 1)
     o = Oracle(m, n + m + 1)
@@ -167,7 +169,7 @@ def test_flush_kernels_block_sizes(lpg, monkeypatch, variant, k, m, n, seed, kin
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("k", [5, 32])
+@pytest.mark.parametrize("k", [5, 32, 40, 64])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1)])
 def test_generic_and_prefetching_pivot_kernels_agree(lpg, monkeypatch, k, m, n, seed, kind, rule):
     """The deferred single-rank pivot runs through k_prep_d / k_select_d; the generic
