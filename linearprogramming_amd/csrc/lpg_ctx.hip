@@ -58,6 +58,8 @@ struct lpg_ctx {
     int64_t logcap = 0;
     DevState *st = nullptr;
     int npp = 0, nsel = 0;
+    int npp_d = 0, nsel_d = 0;    // the same partial counts for the single-rank deferred pair (k_prep_d / k_select_d)
+    int pivot_nt = kPivotThreads; // threads per block of that pair (LPG_PIVOT_NT)
     hipStream_t stream = nullptr;
     bool own_stream = false;
     // pivot-loop host state
@@ -73,6 +75,7 @@ struct lpg_ctx {
     bool capture_block = false;   // capturing a deferred block's pivots (its flush stays outside the graph)
     bool fast_pivot = true;       // deferred single-rank pivots through k_prep_d / k_select_d (LPG_SLOW_PIVOT=1: generic pair)
     double *Pbuf = nullptr, *Cbuf = nullptr;
+    double *zrow = nullptr;       // ld zeros (padding slots of the prefetching pivot kernels)
     int64_t cs = 0;
     int64_t *rq = nullptr;
     int skip = 1;                 // column skipping in the update (LPG_FLAG_NO_SKIP turns it off)
@@ -223,6 +226,7 @@ static Defer defer_of(const lpg_ctx *c, int q) {
     d.basis = c->basis;
     d.logk = c->logk;
     d.logr = c->logr;
+    d.zrow = c->zrow;
     d.q = q;
     d.on = c->defer_k > 0 ? 1 : 0;
     return d;
@@ -255,9 +259,17 @@ static int exchange_candidates(lpg_ctx *c) {
     return comm_allgather(c, c->part, c->cand, sizeof(Cand) * (size_t)c->nsel);
 }
 
+// The generic select of a bootstrap writes nsel ratio candidates, and the
+// deferred pair's k_prep_d reads nsel_d: the rest must read as "none".
+static int clear_candidates(lpg_ctx *c) {
+    if (c->nsel_d > c->nsel)
+        HIPCHK(c, hipMemsetAsync(c->part + c->nsel, 0xff, (size_t)(c->nsel_d - c->nsel) * sizeof(Cand), c->stream));
+    return 0;
+}
+
 static int bootstrap(lpg_ctx *c, int rule) {
     int rc = materialize(c);
-    if (rc) return rc;
+    if (rc || (rc = clear_candidates(c))) return rc;
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
     const Geo g = geo(c);
     if (launch_price(lau(c), g, rule, 0, c->st, 0, c->P, c->C[0], c->pp, c->pc, c->npp))
@@ -276,7 +288,7 @@ static int bootstrap(lpg_ctx *c, int rule) {
 // admits only row r (either sign, |T[r][k]| > eps_piv).
 static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
     int rc = materialize(c);
-    if (rc) return rc;
+    if (rc || (rc = clear_candidates(c))) return rc;
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
     if (launch_select(lau(c), geo(c), rule, true, c->st, 0, 0, c->P, c->C[1], c->C[0], c->pp, c->npp, c->basis,
                       c->part, c->nsel, k, r, c->pc, c->skip, defer_of(c, 0)))
@@ -383,8 +395,8 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
         const bool mark = c->timing && !D.on;   // deferred mode times the flushes only
         if (mark && (rc = timing_mark(c, 0))) return rc;
         if (D.on && fuse && c->fast_pivot) {    // deferred, single rank: the prefetching pair
-            if (launch_pivot_d(L, g, rule, c->st, s, s1, c->part, c->nsel, P, c->C[s], c->C[s1], c->pp, c->npp,
-                               c->basis, D))
+            if (launch_pivot_d(L, g, rule, c->st, s, s1, c->part, c->nsel_d, P, c->C[s], c->C[s1], c->pp, c->npp_d,
+                               c->basis, D, c->pivot_nt))
                 return fail(c, LPG_ERR_DEVICE, "pivot launch failed");
             if (++c->pend == c->defer_k && !c->capture_block)
                 if ((rc = flush_launch(c))) return rc;
@@ -546,7 +558,11 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->npp = price_blocks(g);
     const int64_t maxloc = (m + world - 1) / world + c->nobj;   // identical on every rank
     c->nsel = (int)std::min<int64_t>((maxloc + kBlock - 1) / kBlock, kMaxSelBlocks);
-    if ((int64_t)c->nsel * kBlock < rows) c->fast_pivot = false;   // k_select_d takes one row per thread
+    const char *pn = getenv("LPG_PIVOT_NT");
+    if (pn) c->pivot_nt = atoi(pn) == 128 ? 128 : 256;
+    c->npp_d = pivot_d_blocks(g, 0, c->pivot_nt);
+    c->nsel_d = pivot_d_blocks(g, 1, c->pivot_nt);              // k_select_d: one row per thread
+    if (world > 1) c->fast_pivot = false;
 #define ALLOC(p, bytes)                                                                    \
     do {                                                                                   \
         hipError_t e_ = hipMalloc((void **)&(p), (bytes));                                 \
@@ -564,9 +580,9 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     ALLOC(c->acc, (size_t)c->ld * world * sizeof(double));
     ALLOC(c->cb, (size_t)std::max<int64_t>(c->nloc, 1) * sizeof(double));
     ALLOC(c->cost, (size_t)ncols * sizeof(double));
-    ALLOC(c->pp, (size_t)c->npp * sizeof(PricePart));
+    ALLOC(c->pp, (size_t)std::max(c->npp, c->npp_d) * sizeof(PricePart));
     ALLOC(c->pc, (size_t)c->npp * sizeof(int));
-    ALLOC(c->part, (size_t)c->nsel * sizeof(Cand));
+    ALLOC(c->part, (size_t)std::max(c->nsel, c->nsel_d) * sizeof(Cand));
     if (world > 1) ALLOC(c->cand, (size_t)c->nsel * world * sizeof(Cand));
     else c->cand = c->part;
     ALLOC(c->basis, (size_t)m * sizeof(int64_t));
@@ -578,6 +594,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         ALLOC(c->Pbuf, (size_t)slots * c->ld * sizeof(double));
         ALLOC(c->Cbuf, (size_t)slots * c->cs * sizeof(double));
         ALLOC(c->rq, (size_t)slots * sizeof(int64_t));
+        ALLOC(c->zrow, (size_t)c->ld * sizeof(double));
     }
 #undef ALLOC
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -590,7 +607,8 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     if (hipMemset(c->T, 0, (size_t)rows * c->ld * sizeof(double)) != hipSuccess ||
         hipMemset(c->P, 0, (size_t)c->ld * sizeof(double)) != hipSuccess ||
         hipMemset(c->basis, 0, (size_t)m * sizeof(int64_t)) != hipSuccess ||
-        (c->Cbuf && hipMemset(c->Cbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->cs * sizeof(double)) != hipSuccess)) {
+        (c->Cbuf && hipMemset(c->Cbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->cs * sizeof(double)) != hipSuccess) ||
+        (c->zrow && hipMemset(c->zrow, 0, (size_t)c->ld * sizeof(double)) != hipSuccess)) {
         fail(c, LPG_ERR_DEVICE, "hipMemset failed");
         lpg_destroy(c);
         return LPG_ERR_DEVICE;
@@ -648,7 +666,7 @@ void lpg_destroy(lpg_ctx *c) {
     for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
-                    c->Pbuf, c->Cbuf, c->rq};
+                    c->Pbuf, c->Cbuf, c->rq, c->zrow};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);

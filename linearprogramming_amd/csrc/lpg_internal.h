@@ -60,6 +60,7 @@ struct Defer {
     int64_t  cs;              // Cbuf pitch (>= nloc)
     int64_t *rq;              // K: local pivot row of pivot q, -1 on a non-owner rank
     int64_t *basis, *logk, *logr;   // bookkeeping done by prep_t in deferred mode
+    const double *zrow;       // ld zeros (the padding slots of the prefetching pivot kernels)
     int      q;               // pending index of this pivot
     int      on;
 };
@@ -115,9 +116,14 @@ int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState 
                   const int *pc, int skip, const Defer &D);
 // One deferred-mode pivot without a communicator: k_prep_d + k_select_d
 // (prefetching forms of prep + select; candidates in and out through part).
+// Their grids: pivot_d_blocks(g, 0, nt) prep blocks (= pricing partials),
+// pivot_d_blocks(g, 1, nt) select blocks (= ratio candidates) of nt threads
+// (256 or 128; LPG_PIVOT_NT).
+constexpr int kPivotThreads = 256;
+int pivot_d_blocks(const Geo &g, int which, int nt);
 int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, Cand *part, int nsel,
                    double *P, const double *Cs, double *Cs1, PricePart *pp, int npp, const int64_t *basis,
-                   const Defer &D);
+                   const Defer &D, int nt);
 // Apply the pending pivots (st->npend <= kmax) to constraint rows 0..nloc-1.
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant);
 int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0: k too large)

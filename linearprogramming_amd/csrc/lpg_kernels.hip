@@ -14,6 +14,7 @@
 #include <math.h>
 
 #include <stddef.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -165,6 +166,8 @@ __device__ __forceinline__ int winner_lane(bool mine) {
 }
 
 // == block_reduce_cand for candidates with theta >= 0 and unique keys
+// (NW waves per block; NW == 1: no LDS, no barrier)
+template <int NW = kBlock / 64>
 __device__ Cand block_argmin_cand(const Cand &c) {
     const bool valid = c.row >= 0;
     uint64_t h = valid ? (uint64_t)__double_as_longlong(c.theta) : ~0ull;
@@ -173,29 +176,28 @@ __device__ Cand block_argmin_cand(const Cand &c) {
     const uint32_t ml = l;
     wave_min_key(h, l);
     const int src = winner_lane(valid && mh == h && ml == l);
-    __shared__ Cand sw[kBlock / 64];
+    Cand o{0.0, 0.0, 0, -1};
+    if (src >= 0) {      // wave-uniform
+        o.theta = __longlong_as_double((long long)h);
+        o.key = (int64_t)l;
+        o.piv = __longlong_as_double((long long)rdl64((uint64_t)__double_as_longlong(c.piv), src));
+        o.row = (int64_t)rdl64((uint64_t)c.row, src);
+    }
+    if (NW == 1) return o;
+    __shared__ Cand sw[NW];
     const int w = threadIdx.x >> 6;
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) {
-        Cand o{0.0, 0.0, 0, -1};
-        if (src >= 0) {
-            o.theta = __longlong_as_double((long long)h);
-            o.key = (int64_t)l;
-            o.piv = __longlong_as_double((long long)rdl64((uint64_t)__double_as_longlong(c.piv), src));
-            o.row = (int64_t)rdl64((uint64_t)c.row, src);
-        }
-        sw[w] = o;
-    }
+    if ((threadIdx.x & 63) == 0) sw[w] = o;
     __syncthreads();
     Cand b = sw[0];
 #pragma unroll
-    for (int i = 1; i < kBlock / 64; i++)
+    for (int i = 1; i < NW; i++)
         if (cand_better(sw[i], b)) b = sw[i];
     return b;
 }
 
 // == block_reduce_pp<RULE> for eligible partials (v < 0, unique j)
-template <int RULE>
+template <int RULE, int NW = kBlock / 64>
 __device__ PricePart block_argmin_pp(const PricePart &p) {
     const bool valid = p.j >= 0;
     uint64_t h = ~0ull;
@@ -208,22 +210,21 @@ __device__ PricePart block_argmin_pp(const PricePart &p) {
     const uint32_t ml = l;
     wave_min_key(h, l);
     const int src = winner_lane(valid && mh == h && ml == l);
-    __shared__ PricePart sw[kBlock / 64];
+    PricePart o{0.0, -1, 0, 0};
+    if (src >= 0) {      // wave-uniform
+        o.j = (int64_t)l;
+        o.v = __longlong_as_double((long long)rdl64((uint64_t)__double_as_longlong(p.v), src));
+        o.cls = (int32_t)rdl32((uint32_t)p.cls, src);
+    }
+    if (NW == 1) return o;
+    __shared__ PricePart sw[NW];
     const int w = threadIdx.x >> 6;
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) {
-        PricePart o{0.0, -1, 0, 0};
-        if (src >= 0) {
-            o.j = (int64_t)l;
-            o.v = __longlong_as_double((long long)rdl64((uint64_t)__double_as_longlong(p.v), src));
-            o.cls = (int32_t)rdl32((uint32_t)p.cls, src);
-        }
-        sw[w] = o;
-    }
+    if ((threadIdx.x & 63) == 0) sw[w] = o;
     __syncthreads();
     PricePart b = sw[0];
 #pragma unroll
-    for (int i = 1; i < kBlock / 64; i++)
+    for (int i = 1; i < NW; i++)
         if (pp_better<RULE>(sw[i], b)) b = sw[i];
     return b;
 }
@@ -814,11 +815,11 @@ __device__ unsigned long long g_ph[2][16];
 #define LPG_PH(kern, k) do { } while (0)
 #endif
 
-template <int RULE, int kPF>
-__global__ __launch_bounds__(kBlock) void k_prep_d(double *__restrict__ T, Geo g, DevState *st, int s,
+template <int RULE, int kPF, int NT>
+__global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, DevState *st, int s,
                                                    const Cand *__restrict__ cand, int ncand, double *__restrict__ P,
                                                    const double *__restrict__ Cs, PricePart *__restrict__ pp, Defer D) {
-    const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t j2 = (int64_t)blockIdx.x * NT + threadIdx.x;
     const int64_t nvec = (g.ncols + 1) / 2;
     const bool col = j2 < nvec;
     const int64_t rM = g.nloc, rR = g.nloc + g.nobj - 1;
@@ -827,7 +828,7 @@ __global__ __launch_bounds__(kBlock) void k_prep_d(double *__restrict__ T, Geo g
     // ---- round 1: nothing here depends on the leaving row
     const int32_t status = st->slot[s].status;
     Cand best{0.0, 0.0, 0, -1};
-    for (int q = threadIdx.x; q < ncand; q += kBlock) {
+    for (int q = threadIdx.x; q < ncand; q += NT) {
         const Cand c = cand[q];
         if (cand_better(c, best)) best = c;
     }
@@ -838,14 +839,19 @@ __global__ __launch_bounds__(kBlock) void k_prep_d(double *__restrict__ T, Geo g
     }
     const double cM = -Cs[rM], cR = -Cs[rR];
     const int npf = D.q < kPF ? D.q : kPF;
+    // slots past the block are (+0, +0) and their multiplier is -0: the chain
+    // step fma(-0, +0, x) == x for every x, so the loop below needs no bound
+    // (slots past the block load from an all-zero row: no branch and no
+    // select per load, either of which makes the 64 loads wait in turn)
     d2 pq[kPF];
+    const int64_t jc = col ? 2 * j2 : 0;
 #pragma unroll
     for (int u = 0; u < kPF; u++)
-        if (u < npf && col) pq[u] = *(const d2 *)(D.Pbuf + (int64_t)u * g.ld + 2 * j2);
+        pq[u] = *(const d2 *)((u < npf ? D.Pbuf + (int64_t)u * g.ld : D.zrow) + jc);
     const int64_t rqv = lane < D.q ? D.rq[lane] : -1;   // lane q of every wave holds r_q
     if (status != RUNNING) return;
     LPG_PH(0, 1);
-    best = block_argmin_cand(best);
+    best = block_argmin_cand<NT / 64>(best);
     LPG_PH(0, 2);
     if (best.row < 0 || !isfinite(best.piv) || !isfinite(best.theta)) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -876,35 +882,45 @@ __global__ __launch_bounds__(kBlock) void k_prep_d(double *__restrict__ T, Geo g
     // the multiplier read back from lane q (v_readlane: no LDS, no barrier)
     d2 t = d2{0.0, 0.0};
     if (col) t = *(const d2 *)(T + rl * g.ld + 2 * j2);
-    const double cl = lane < D.q ? -D.Cbuf[(int64_t)lane * D.cs + rl] : 0.0;
+    const double cl = lane < D.q ? -D.Cbuf[(int64_t)lane * D.cs + rl] : -0.0;
     const unsigned long long hit = __ballot(lane < D.q && rqv == rl);
     const int qs = hit ? 63 - __clzll((long long)hit) : -1;
     LPG_PH(0, 3);
     PricePart pbest{0.0, -1, 0, 0};
     const uint64_t clb = (uint64_t)__double_as_longlong(cl);
-    if (col) {
+    // The chain runs in every lane (EXEC full, uniform branches only): a
+    // readlane returns the source lane's register whether or not that lane
+    // was active when the register was written, so the multipliers must never
+    // sit behind a per-lane condition. Straight-line steps: a uniform branch
+    // per step cost ~100 cycles on a lone wave; the common case has no
+    // restart on this row.
+    if (qs < 0) {
 #pragma unroll
         for (int u = 0; u < kPF; u++) {
-            if (u < npf) {
-                if (u == qs) {
-                    t = pq[u];
-                } else if (u > qs) {
-                    const double c = __longlong_as_double((long long)rdl64(clb, u));
-                    t.x = fma(c, pq[u].x, t.x);
-                    t.y = fma(c, pq[u].y, t.y);
-                }
-            }
+            const double c = __longlong_as_double((long long)rdl64(clb, u));
+            t.x = fma(c, pq[u].x, t.x);
+            t.y = fma(c, pq[u].y, t.y);
         }
-        for (int q = kPF; q < D.q; q++) {       // blocks longer than kPF
-            const d2 v = *(const d2 *)(D.Pbuf + (int64_t)q * g.ld + 2 * j2);
-            if (q == qs) {
-                t = v;
-            } else if (q > qs) {
-                const double c = __longlong_as_double((long long)rdl64(clb, q));
-                t.x = fma(c, v.x, t.x);
-                t.y = fma(c, v.y, t.y);
-            }
+    } else {
+#pragma unroll
+        for (int u = 0; u < kPF; u++) {
+            const double c = __longlong_as_double((long long)rdl64(clb, u));
+            const double fx = fma(c, pq[u].x, t.x), fy = fma(c, pq[u].y, t.y);
+            t.x = u == qs ? pq[u].x : (u > qs ? fx : t.x);
+            t.y = u == qs ? pq[u].y : (u > qs ? fy : t.y);
         }
+    }
+    for (int q = kPF; q < D.q; q++) {       // blocks longer than kPF (the launcher avoids them)
+        const d2 v = col ? *(const d2 *)(D.Pbuf + (int64_t)q * g.ld + 2 * j2) : d2{0.0, 0.0};
+        const double c = __longlong_as_double((long long)rdl64(clb, q));
+        if (q == qs) {
+            t = v;
+        } else if (q > qs) {
+            t.x = fma(c, v.x, t.x);
+            t.y = fma(c, v.y, t.y);
+        }
+    }
+    if (col) {
         const double piv = best.piv;
         d2 p;
         p.x = t.x / piv;
@@ -920,19 +936,19 @@ __global__ __launch_bounds__(kBlock) void k_prep_d(double *__restrict__ T, Geo g
         price_one<RULE>(pbest, dM.y, dR.y, 2 * j2 + 1, g);
     }
     LPG_PH(0, 4);
-    pbest = block_argmin_pp<RULE>(pbest);
+    pbest = block_argmin_pp<RULE, NT / 64>(pbest);
     if (threadIdx.x == 0) pp[blockIdx.x] = pbest;
     LPG_PH(0, 5);
 }
 
-template <int RULE, int kPF>
-__global__ __launch_bounds__(kBlock) void k_select_d(const double *__restrict__ T, Geo g, DevState *st, int s,
+template <int RULE, int kPF, int NT>
+__global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, Geo g, DevState *st, int s,
                                                      int s1, const double *__restrict__ Cs, double *__restrict__ Cs1,
                                                      const PricePart *__restrict__ pp, int npp,
                                                      const int64_t *__restrict__ basis, Cand *__restrict__ part,
                                                      Defer D) {
     const int64_t nrows = g.nloc + g.nobj;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;   // one row per thread (launcher checks)
+    const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;   // one row per thread (launcher checks)
     const bool row = i < nrows;
     const bool crow = i < g.nloc;
     const int lane = threadIdx.x & 63;
@@ -941,7 +957,7 @@ __global__ __launch_bounds__(kBlock) void k_select_d(const double *__restrict__ 
     const int32_t stt = st->slot[s].status;
     const int64_t r = st->slot[s].r, kc = st->slot[s].k;
     PricePart pb{0.0, -1, 0, 0};
-    for (int q = threadIdx.x; q < npp; q += kBlock) {
+    for (int q = threadIdx.x; q < npp; q += NT) {
         const PricePart c = pp[q];
         if (pp_better<RULE>(c, pb)) pb = c;
     }
@@ -951,10 +967,12 @@ __global__ __launch_bounds__(kBlock) void k_select_d(const double *__restrict__ 
         csi = Cs[i];
     }
     const int npf = D.q < kPF ? D.q : kPF;
-    double cv[kPF];
+    double cv[kPF];                  // slots past the pending block: +0 (with P entries +0 below: no-op steps)
 #pragma unroll
-    for (int u = 0; u < kPF; u++)
+    for (int u = 0; u < kPF; u++) {
+        cv[u] = 0.0;
         if (u < npf && crow) cv[u] = D.Cbuf[(int64_t)u * D.cs + i];
+    }
     // lane q of every wave holds P_q[0], r_q (q <= D.q: pivot t included)
     const bool lq = lane <= D.q;
     const double p0l = lq ? D.Pbuf[(int64_t)lane * g.ld] : 0.0;
@@ -971,7 +989,7 @@ __global__ __launch_bounds__(kBlock) void k_select_d(const double *__restrict__ 
     }
     if (crow) D.Cbuf[(int64_t)D.q * D.cs + i] = csi;   // pivot t is pending: its column C_t
     LPG_PH(1, 1);
-    pb = block_argmin_pp<RULE>(pb);
+    pb = block_argmin_pp<RULE, NT / 64>(pb);
     LPG_PH(1, 2);
     if (pb.j < 0) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -993,49 +1011,62 @@ __global__ __launch_bounds__(kBlock) void k_select_d(const double *__restrict__ 
     LPG_PH(1, 3);
     const uint64_t p0b = (uint64_t)__double_as_longlong(p0l), pkb = (uint64_t)__double_as_longlong(pkl);
     Cand best{0.0, 0.0, 0, -1};
-    if (row) {
-        double b = ob, a = oa;
-        if (crow) {                   // columns 0 and k_{t+1}: chain over pivots 0..q
-            const int32_t ii = (int32_t)i;
+    // columns 0 and k_{t+1}: the chain over pivots 0..q, in EVERY lane (rows
+    // past the tableau and objective rows compute junk that is dropped below):
+    // a readlane returns the source lane's register whether or not that lane
+    // was active when it was written, so no chain input may be computed behind
+    // a per-lane condition
+    double b = ob, a = oa;
+    const int32_t ii = (int32_t)i;
+    if (D.q <= kPF) {
+        // straight line over kPF slots: lanes >= D.q read as (P = +0, r = -1)
+        // and cv = +0 there, so those steps are fma(-0, +0, x) == x
+        const bool lp = lane < D.q;
+        const uint64_t p0m = lp ? p0b : 0ull, pkm = lp ? pkb : 0ull;
+        const uint32_t rqm = lp ? (uint32_t)rql : 0xffffffffu;
 #pragma unroll
-            for (int u = 0; u < kPF; u++) {
-                if (u < npf) {
-                    const double q0 = __longlong_as_double((long long)rdl64(p0b, u));
-                    const double qk = __longlong_as_double((long long)rdl64(pkb, u));
-                    if (ii == (int32_t)rdl32((uint32_t)rql, u)) {
-                        b = q0;
-                        a = qk;
-                    } else {
-                        b = fma(-cv[u], q0, b);
-                        a = fma(-cv[u], qk, a);
-                    }
-                }
-            }
-            for (int q = kPF; q <= D.q; q++) {   // the rest of a long block, and pivot t itself
-                const double q0 = __longlong_as_double((long long)rdl64(p0b, q));
-                const double qk = __longlong_as_double((long long)rdl64(pkb, q));
-                const double c = q == D.q ? -csi : -D.Cbuf[(int64_t)q * D.cs + i];
-                if (ii == (int32_t)rdl32((uint32_t)rql, q)) {
-                    b = q0;
-                    a = qk;
-                } else {
-                    b = fma(c, q0, b);
-                    a = fma(c, qk, a);
-                }
-            }
-            if (D.q < kPF) {          // pivot t itself: C_t is Cs
-                const int q = D.q;
-                const double q0 = __longlong_as_double((long long)rdl64(p0b, q));
-                const double qk = __longlong_as_double((long long)rdl64(pkb, q));
-                if (ii == (int32_t)rdl32((uint32_t)rql, q)) {
-                    b = q0;
-                    a = qk;
-                } else {
-                    b = fma(-csi, q0, b);
-                    a = fma(-csi, qk, a);
-                }
-            }
-        }                             // objective rows are current (prep wrote d_{t+1})
+        for (int u = 0; u < kPF; u++) {
+            const double q0 = __longlong_as_double((long long)rdl64(p0m, u));
+            const double qk = __longlong_as_double((long long)rdl64(pkm, u));
+            const bool hit = ii == (int32_t)rdl32(rqm, u);
+            const double fb = fma(-cv[u], q0, b), fa = fma(-cv[u], qk, a);
+            b = hit ? q0 : fb;
+            a = hit ? qk : fa;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < kPF; u++) {
+            const double q0 = __longlong_as_double((long long)rdl64(p0b, u));
+            const double qk = __longlong_as_double((long long)rdl64(pkb, u));
+            const bool hit = ii == (int32_t)rdl32((uint32_t)rql, u);
+            const double fb = fma(-cv[u], q0, b), fa = fma(-cv[u], qk, a);
+            b = hit ? q0 : fb;
+            a = hit ? qk : fa;
+        }
+    }
+    for (int q = kPF; q <= D.q; q++) {   // the rest of a long block, and pivot t itself
+        const double q0 = __longlong_as_double((long long)rdl64(p0b, q));
+        const double qk = __longlong_as_double((long long)rdl64(pkb, q));
+        const double c = q == D.q ? -csi : (crow ? -D.Cbuf[(int64_t)q * D.cs + i] : -0.0);
+        const bool hit = ii == (int32_t)rdl32((uint32_t)rql, q);
+        const double fb = fma(c, q0, b), fa = fma(c, qk, a);
+        b = hit ? q0 : fb;
+        a = hit ? qk : fa;
+    }
+    if (D.q < kPF) {          // pivot t itself: C_t is Cs
+        const int q = D.q;
+        const double q0 = __longlong_as_double((long long)rdl64(p0b, q));
+        const double qk = __longlong_as_double((long long)rdl64(pkb, q));
+        const bool hit = ii == (int32_t)rdl32((uint32_t)rql, q);
+        const double fb = fma(-csi, q0, b), fa = fma(-csi, qk, a);
+        b = hit ? q0 : fb;
+        a = hit ? qk : fa;
+    }
+    if (!crow) {              // objective rows are current (prep wrote d_{t+1})
+        b = ob;
+        a = oa;
+    }
+    if (row) {
         Cs1[i] = a;
         if (crow && a > g.eps_piv) {
             const int64_t grow = g.row0 + i;
@@ -1048,7 +1079,7 @@ __global__ __launch_bounds__(kBlock) void k_select_d(const double *__restrict__ 
         }
     }
     LPG_PH(1, 4);
-    best = block_argmin_cand(best);
+    best = block_argmin_cand<NT / 64>(best);
     if (threadIdx.x == 0) part[blockIdx.x] = best;
     LPG_PH(1, 5);
 }
@@ -1066,26 +1097,39 @@ int debug_phases(unsigned long long *out, int reset) {
 }
 #endif
 
+int pivot_d_blocks(const Geo &g, int which, int nt) {
+    return which == 0 ? (int)(((g.ncols + 1) / 2 + nt - 1) / nt) : (int)((g.nloc + g.nobj + nt - 1) / nt);
+}
+
 int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, Cand *part, int nsel,
                    double *P, const double *Cs, double *Cs1, PricePart *pp, int npp, const int64_t *basis,
-                   const Defer &D) {
-    if ((int64_t)nsel * kBlock < g.nloc + g.nobj) return -1;   // k_select_d: one row per thread
+                   const Defer &D, int nt) {
+    // nt = 128 spreads the prefetch of the pending rows over twice the CUs
+    // (measured: no gain at config 3, 20.2 vs 20.4 us per pivot). One-wave
+    // blocks (nt = 64) gave wrong pivot rows at m >= 8192 and are not offered.
+    if ((nt != 128 && nt != 256) || npp != pivot_d_blocks(g, 0, nt) || nsel != pivot_d_blocks(g, 1, nt)) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
-#define LPG_PD(R, PF)                                                                                             \
-    do {                                                                                                          \
-        hipLaunchKernelGGL((k_prep_d<R, PF>), dim3(npp), dim3(kBlock), 0, stream, g.T, g, st, s, part, nsel, P, Cs, \
-                           pp, D);                                                                                \
-        hipLaunchKernelGGL((k_select_d<R, PF>), dim3(nsel), dim3(kBlock), 0, stream, g.T, g, st, s, s1, Cs, Cs1,   \
-                           pp, npp, basis, part, D);                                                              \
+#define LPG_PD(R, PF, NT)                                                                                             \
+    do {                                                                                                              \
+        hipLaunchKernelGGL((k_prep_d<R, PF, NT>), dim3(npp), dim3(NT), 0, stream, g.T, g, st, s, part, nsel, P, Cs, pp, \
+                           D);                                                                                        \
+        hipLaunchKernelGGL((k_select_d<R, PF, NT>), dim3(nsel), dim3(NT), 0, stream, g.T, g, st, s, s1, Cs, Cs1, pp,   \
+                           npp, basis, part, D);                                                                      \
+    } while (0)
+#define LPG_PD_NT(R, PF)                   \
+    do {                                   \
+        if (nt == 128) LPG_PD(R, PF, 128); \
+        else LPG_PD(R, PF, 256);           \
     } while (0)
     const bool wide = D.q >= 32;            // pending chain longer than 32: the 64-slot prefetch forms
     if (rule == RULE_BLAND) {
-        if (wide) LPG_PD(RULE_BLAND, 64);
-        else LPG_PD(RULE_BLAND, 32);
+        if (wide) LPG_PD_NT(RULE_BLAND, 64);
+        else LPG_PD_NT(RULE_BLAND, 32);
     } else {
-        if (wide) LPG_PD(RULE_DANTZIG, 64);
-        else LPG_PD(RULE_DANTZIG, 32);
+        if (wide) LPG_PD_NT(RULE_DANTZIG, 64);
+        else LPG_PD_NT(RULE_DANTZIG, 32);
     }
+#undef LPG_PD_NT
 #undef LPG_PD
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

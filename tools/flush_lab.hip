@@ -121,22 +121,18 @@ __global__ __launch_bounds__(kBlock) void k_flushr(double *__restrict__ T, Geo g
     if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
 }
 
-// k_flushw: k_flushm's wave tile (16 rows x 32 columns, 16-byte accesses,
-// even/odd-column MFMA chains, B fragments in VGPRs) on tall items: a block's
-// 4 waves sweep R rows of a 128-column tile in 16-row bands, in step. The
-// multipliers of band s (-C_q[i], fragment order [q][row]) sit in an NB-deep
-// LDS ring, loaded into registers one band ahead and written one barrier
-// later; the tableau band s+1 is loaded while band s is on the matrix cores.
-template <int KMAX, int R, int NB, int LB>
-__global__ __launch_bounds__(kBlock, LB) void k_flushw(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+template <int KMAX, int NB, int LB>
+__global__ __launch_bounds__(kBlock, LB) void k_flushw2(double *__restrict__ T, Geo g, DevState *__restrict__ st,
                                                        const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
-                                                       int64_t cs, int64_t ntiles, int64_t nitems, int skip) {
+                                                       int64_t cs, int64_t ntiles, int64_t nitems, int64_t rows,
+                                                       int skip) {
     constexpr int G = KMAX / 4;
     constexpr int BAND = KMAX * 16;                 // doubles per band
-    constexpr int PER = BAND / 2 / kBlock;          // 16-byte C pieces per thread per band
+    constexpr int PER = BAND / 2 / kBlock;          // 16-byte multiplier pieces per thread per band
     static_assert(PER >= 1 && BAND / 2 % kBlock == 0, "band staging");
     __shared__ __attribute__((aligned(16))) double sC[NB][BAND];
     __shared__ int64_t next_item;
+    __shared__ int wsum[kBlock / 64];
     const int np = (int)st->npend;
     if (np <= 0) return;
     const int64_t ld = g.ld;
@@ -150,11 +146,10 @@ __global__ __launch_bounds__(kBlock, LB) void k_flushw(double *__restrict__ T, G
         const int64_t item = next_item;
         if (item >= nitems) break;
         const int64_t tile = item % ntiles, strip = item / ntiles;
-        const int64_t i0 = strip * R;
-        const int64_t i1 = i0 + R < g.nloc ? i0 + R : g.nloc;
-        const int64_t c0 = tile * 128 + wave * 32;
-        const int64_t cl = c0 + 2 * lc;
-        const bool in = cl < g.ncols;
+        const int64_t i0 = strip * rows;
+        const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
+        const int64_t cl = tile * 128 + wave * 32 + 2 * lc;   // this lane's column pair
+        const bool in = cl < g.ncols;                         // cl even, ld even: cl + 1 < ld
         double be[G], bo[G];
         bool live = false;
 #pragma unroll
@@ -166,24 +161,29 @@ __global__ __launch_bounds__(kBlock, LB) void k_flushw(double *__restrict__ T, G
             bo[gq] = v.y;
             live = live || v.x != 0.0 || v.y != 0.0;
         }
+        // a column pair is live if any of its P entries over all slots is
+        // non-zero: OR over the 4 lanes holding its k-slices
         live = (__shfl_xor((int)live, 16, 64) | (int)live) != 0;
         live = (__shfl_xor((int)live, 32, 64) | (int)live) != 0;
         const bool ok = in && (!skip || live);
-        const int nlive = ok ? (cl + 1 < g.ncols ? 2 : 1) : 0;
-        int mine = lk == 0 ? nlive : 0;
-        for (int mask = 32; mask > 0; mask >>= 1) mine += __shfl_xor(mine, mask, 64);
-        const bool wlive = mine > 0;                    // wave-uniform
-        const int cnt = __syncthreads_count(wlive && lane == 0 ? 1 : 0);
-        if (cnt == 0) continue;
-        {
-            __shared__ int wsum[kBlock / 64];
-            if (lane == 0) wsum[wave] = mine;
-            __syncthreads();
-            if (threadIdx.x == 0)
-                touched += (unsigned long long)(wsum[0] + wsum[1] + wsum[2] + wsum[3]) * (unsigned long long)(i1 - i0);
+        // per-chain liveness: the even (odd) chain runs if any even (odd) column of the wave is live
+        bool le = false, lo = false;
+#pragma unroll
+        for (int gq = 0; gq < G; gq++) {
+            le = le || be[gq] != 0.0;
+            lo = lo || bo[gq] != 0.0;
         }
+        const bool run_e = !skip || __ballot(in && le) != 0, run_o = !skip || __ballot(in && lo && cl + 1 < g.ncols) != 0;
+        int mine = (lk == 0 && ok) ? (cl + 1 < g.ncols ? 2 : 1) : 0;   // live doubles per row, pairs counted once
+        for (int mask = 32; mask > 0; mask >>= 1) mine += __shfl_xor(mine, mask, 64);
+        const bool wlive = mine > 0;                                   // wave-uniform
+        if (lane == 0) wsum[wave] = mine;
+        if (__syncthreads_count(wlive && lane == 0) == 0) continue;    // the whole tile is skipped
+        if (threadIdx.x == 0)
+            touched += (unsigned long long)(wsum[0] + wsum[1] + wsum[2] + wsum[3]) * (unsigned long long)(i1 - i0);
         const int nb = (int)((i1 - i0 + 15) / 16);
-        // C piece e of band s: slot q = e / 8, rows 2 (e % 8) .. +1 of the band
+        // multiplier piece e of band s: slot q = e / 8, band rows 2 (e % 8) .. +1
+        // (zeros past np and past i1: A = -0 there, x + -0 == x)
         auto cload = [&](d2 (&cr)[PER], int s) {
 #pragma unroll
             for (int u = 0; u < PER; u++) {
@@ -191,56 +191,58 @@ __global__ __launch_bounds__(kBlock, LB) void k_flushw(double *__restrict__ T, G
                 const int q = e >> 3, rr = 2 * (e & 7);
                 const int64_t row = i0 + 16 * s + rr;
                 d2 v = d2{0.0, 0.0};
-                if (s < nb && q < np && row < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + row);
+                if (s < nb && q < np && row < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + row);   // row + 1 < cs
                 cr[u] = -v;
             }
         };
         auto cstore = [&](const d2 (&cr)[PER], int s) {
 #pragma unroll
-            for (int u = 0; u < PER; u++) {
-                const int e = threadIdx.x + u * kBlock;
-                *(d2 *)(&sC[s % NB][2 * e]) = cr[u];
-            }
+            for (int u = 0; u < PER; u++) *(d2 *)(&sC[s % NB][2 * (threadIdx.x + u * kBlock)]) = cr[u];
         };
-        // prologue: bands 0 .. NB-2 into the ring, band NB-1 into registers
-        for (int s = 0; s < NB - 1; s++) {
+        for (int s = 0; s < NB - 1; s++) {   // prologue: bands 0 .. NB-2 into the ring
             d2 cr[PER];
             cload(cr, s);
             cstore(cr, s);
         }
         d2 cn[PER];
         cload(cn, NB - 1);
-        d2 t[4];
         auto tload = [&](d2 (&x)[4], int s) {
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int64_t row = i0 + 16 * s + lk + 4 * r;
-                const d2 *a = (const d2 *)(T + row * ld + cl);
-                x[r] = (wlive && ok && row < i1) ? __builtin_nontemporal_load(a) : d2{0.0, 0.0};
+                x[r] = (ok && row < i1) ? __builtin_nontemporal_load((const d2 *)(T + row * ld + cl)) : d2{0.0, 0.0};
             }
         };
+        d2 t[4];
         tload(t, 0);
         for (int s = 0; s < nb; s++) {
             d2 tn[4];
             if (s + 1 < nb) tload(tn, s + 1);
-            __syncthreads();                      // band s staged; buffer (s - 1) % NB free
+            __syncthreads();                  // band s is staged; ring slot (s - 1) % NB is free
             cstore(cn, s + NB - 1);
             cload(cn, s + NB);
             if (wlive) {
                 d4 ae = d4{t[0].x, t[1].x, t[2].x, t[3].x};
                 d4 ao = d4{t[0].y, t[1].y, t[2].y, t[3].y};
                 const double *sa = &sC[s % NB][lk * 16 + lc];
+                if (run_e && run_o) {
 #pragma unroll
-                for (int gq = 0; gq < G; gq++) {
-                    const double a = sa[gq * 64];
-                    ae = __builtin_amdgcn_mfma_f64_16x16x4f64(a, be[gq], ae, 0, 0, 0);
-                    ao = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bo[gq], ao, 0, 0, 0);
+                    for (int gq = 0; gq < G; gq++) {
+                        const double a = sa[gq * 64];
+                        ae = __builtin_amdgcn_mfma_f64_16x16x4f64(a, be[gq], ae, 0, 0, 0);
+                        ao = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bo[gq], ao, 0, 0, 0);
+                    }
+                } else if (run_e) {
+#pragma unroll
+                    for (int gq = 0; gq < G; gq++) ae = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[gq * 64], be[gq], ae, 0, 0, 0);
+                } else {
+#pragma unroll
+                    for (int gq = 0; gq < G; gq++) ao = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[gq * 64], bo[gq], ao, 0, 0, 0);
                 }
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int64_t row = i0 + 16 * s + lk + 4 * r;
-                    if (ok && row < i1)
-                        __builtin_nontemporal_store(d2{ae[r], ao[r]}, (d2 *)(T + row * ld + cl));
+                    if (ok && row < i1) __builtin_nontemporal_store(d2{ae[r], ao[r]}, (d2 *)(T + row * ld + cl));
                 }
             }
 #pragma unroll
@@ -264,10 +266,14 @@ __global__ void k_fill(double *x, int64_t n, uint64_t seed) {
     }
 }
 
-// P_q[j] = 0 for the slack block and the padding (the skipped columns)
-__global__ void k_zero_cols(double *P, int64_t ld, int64_t j0, int k) {
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)k * ld; e += (int64_t)gridDim.x * blockDim.x)
-        if (e % ld >= j0) P[e] = 0.0;
+// P_q[j] = 0 for the slack block and the padding (the skipped columns),
+// except every `every`-th slack column (0: none), which stays live: the
+// slacks that left the basis, scattered over the block as in a real solve
+__global__ void k_zero_cols(double *P, int64_t ld, int64_t j0, int64_t j1, int k, int64_t every) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)k * ld; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = e % ld;
+        if (j >= j0 && !(every > 0 && j < j1 && (j - j0) % every == 0)) P[e] = 0.0;
+    }
 }
 
 __global__ void k_cmp(const double *a, const double *b, int64_t n, unsigned long long *bad) {
@@ -357,8 +363,17 @@ static void fn_w(Lab &L) {
     const int64_t ntiles = (L.g.ncols + 127) / 128;
     const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
     const int64_t nblocks = std::min<int64_t>(nitems, 256 * PERCU);
-    hipLaunchKernelGGL((k_flushw<KMAX, R, NB, LB>), dim3((unsigned)nblocks), dim3(kBlock), 0, 0, L.g.T, L.g, L.st,
-                       L.D.Pbuf, L.D.Cbuf, L.D.cs, ntiles, nitems, 1);
+    hipLaunchKernelGGL((k_flushw<KMAX, NB, LB>), dim3((unsigned)nblocks), dim3(kBlock), 0, 0, L.g.T, L.g, L.st,
+                       L.D.Pbuf, L.D.Cbuf, L.D.cs, ntiles, nitems, (int64_t)R, 1);
+}
+
+template <int KMAX, int R, int NB, int LB, int PERCU>
+static void fn_w2(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 127) / 128;
+    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
+    const int64_t nblocks = std::min<int64_t>(nitems, 256 * PERCU);
+    hipLaunchKernelGGL((k_flushw2<KMAX, NB, LB>), dim3((unsigned)nblocks), dim3(kBlock), 0, 0, L.g.T, L.g, L.st,
+                       L.D.Pbuf, L.D.Cbuf, L.D.cs, ntiles, nitems, (int64_t)R, 1);
 }
 
 int main(int argc, char **argv) {
@@ -382,7 +397,8 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, L.T0, L.n, 1ull);
     hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, Pbuf, (int64_t)64 * ld, 2ull);
     hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, Cbuf, (int64_t)64 * cs, 3ull);
-    hipLaunchKernelGGL(k_zero_cols, dim3(1024), dim3(256), 0, 0, Pbuf, ld, nstruct + 1, 64);
+    const int64_t every = getenv("LAB_SCATTER") ? atoll(getenv("LAB_SCATTER")) : 0;
+    hipLaunchKernelGGL(k_zero_cols, dim3(1024), dim3(256), 0, 0, Pbuf, ld, nstruct + 1, ncols, 64, every);
     CHK(hipDeviceSynchronize());
     L.g.T = L.T;
     L.g.ld = ld;
@@ -398,8 +414,8 @@ int main(int argc, char **argv) {
     L.D.on = 1;
     CHK(hipEventCreate(&L.e0));
     CHK(hipEventCreate(&L.e1));
-    printf("flush lab: %lld rows x %lld cols (ld %lld), K=%d, P zero for columns > %lld\n", (long long)m,
-           (long long)ncols, (long long)ld, L.K, (long long)nstruct);
+    printf("flush lab: %lld rows x %lld cols (ld %lld), K=%d, P zero for columns > %lld except every %lld-th\n",
+           (long long)m, (long long)ncols, (long long)ld, L.K, (long long)nstruct, (long long)every);
     // reference result: the engine's default flush
     CHK(hipMemcpy(L.T, L.T0, L.n * 8, hipMemcpyDeviceToDevice));
     L.reset_state();
@@ -429,7 +445,8 @@ int main(int argc, char **argv) {
     if (L.K <= 32) {
         W(32, 512, 2, 3, 3) W(32, 512, 3, 3, 3) W(32, 256, 2, 3, 3) W(32, 1024, 2, 3, 3) W(32, 512, 2, 4, 4)
     } else {
-        W(64, 512, 2, 3, 3) W(64, 512, 3, 3, 3) W(64, 256, 2, 3, 3) W(64, 1024, 2, 3, 3) W(64, 512, 2, 2, 2)
+        W(64, 512, 2, 2, 2) W(64, 512, 3, 2, 2) W(64, 256, 2, 2, 2) W(64, 1024, 2, 2, 2)
     }
+    if (L.K > 32 && want("w2<64,512,2,2,2>")) run(L, fn_w2<64, 512, 2, 2, 2>, "w2<64,512,2,2,2>", true, reps);
     return 0;
 }

@@ -21,17 +21,18 @@ lib.lpg_debug_phases.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_in
 m, n = int(os.environ.get("M", 16384)), int(os.environ.get("N", 32768))
 e = lpg.Engine(m, n + m + 1)
 e.generate(n, 20220518, 0)
-e.reserve_log(200)
-e.solve(33, 0)                       # warm: bootstrap + one block, flushed
+K = e.info.defer_k
+e.reserve_log(3 * K + 8)
+e.solve(K + 1, 0)                    # warm: bootstrap + one block, flushed
 buf = (ctypes.c_ulonglong * 32)()
 names = {0: ["start", "status", "cand-reduce", "row2-staged", "chain+P+price", "pp-reduce"],
          1: ["start", "status", "pp-reduce", "staged", "chain", "cand-reduce"]}
-for q in range(32):
+for q in range(K):
     lib.lpg_debug_phases(buf, 1)
     e.enqueue(1, 0)
     torch.cuda.synchronize()
     lib.lpg_debug_phases(buf, 0)
-    if q in (0, 1, 8, 16, 31):
+    if q in (0, 1, 16, K // 2 - 1, K // 2, 3 * K // 4, K - 1):
         for kern in (0, 1):
             ph = [buf[kern * 16 + j] for j in range(16)]
             t0 = ph[14]
