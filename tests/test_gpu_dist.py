@@ -86,10 +86,10 @@ def lpg():
     return lpg
 
 
-@pytest.mark.parametrize("defer", [None, "0", "5"])
+@pytest.mark.parametrize("defer", [None, "0", "5", "64"])
 @pytest.mark.parametrize("world,m,n,kind,rule", [(2, 96, 160, 0, 0), (3, 101, 77, 0, 0), (2, 64, 64, 1, 1)])
 def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule, defer, monkeypatch):
-    """Row blocks over ranks; default deferred blocks, eager (0) and 5-pivot blocks."""
+    """Row blocks over ranks; default deferred blocks, eager (0), 5- and 64-pivot blocks."""
     if defer is not None:
         monkeypatch.setenv("LPG_DEFER", defer)
     seed = 777
@@ -159,11 +159,13 @@ def test_two_processes_gloo_bitwise(lpg):
     assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
 
 
-@pytest.mark.parametrize("m,n", [(300, 500), (1024, 2048)])
-def test_rccl_single_rank_communicator(lpg, m, n):
+@pytest.mark.parametrize("m,n,defer", [(300, 500, None), (1024, 2048, None), (1024, 2048, "64")])
+def test_rccl_single_rank_communicator(lpg, m, n, defer, monkeypatch):
     """The RCCL transport on a 1-rank communicator: every per-pivot ncclAllReduce
     (pivot row) and ncclAllGather (ratio candidates) really runs, and the result
     is bitwise the engine without a communicator (and the oracle)."""
+    if defer is not None:
+        monkeypatch.setenv("LPG_DEFER", defer)
     e = lpg.Engine(m, n + m + 1)
     e.comm_init_rccl(lpg.Engine.rccl_unique_id())
     e.generate(n, 41, 0)
