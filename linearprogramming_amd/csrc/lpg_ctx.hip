@@ -76,6 +76,12 @@ struct lpg_ctx {
     bool fast_pivot = true;       // deferred single-rank pivots through k_prep_d / k_select_d (LPG_SLOW_PIVOT=1: generic pair)
     double *Pbuf = nullptr, *Cbuf = nullptr;
     double *zrow = nullptr;       // ld zeros (padding slots of the prefetching pivot kernels)
+    // basis-partitioned column order (single-rank deferred path, lpg_internal.h)
+    int64_t *kq = nullptr, *lv = nullptr;   // per pending pivot: entering / leaving variable
+    int32_t *colmap = nullptr, *inv = nullptr, *pairs = nullptr;
+    double *tmp = nullptr;        // row chunk for canonicalize()
+    int64_t tmp_rows = 0;
+    bool permuted = false;        // colmap may differ from the identity
     int64_t cs = 0;
     int64_t *rq = nullptr;
     int skip = 1;                 // column skipping in the update (LPG_FLAG_NO_SKIP turns it off)
@@ -227,6 +233,9 @@ static Defer defer_of(const lpg_ctx *c, int q) {
     d.logk = c->logk;
     d.logr = c->logr;
     d.zrow = c->zrow;
+    d.kq = c->kq;
+    d.lv = c->lv;
+    d.colmap = c->colmap;
     d.q = q;
     d.on = c->defer_k > 0 ? 1 : 0;
     return d;
@@ -235,11 +244,20 @@ static Defer defer_of(const lpg_ctx *c, int q) {
 // Apply the pending block (its size on the device is st->npend <= pend).
 // In deferred mode the timing ring brackets exactly this (k_flush +
 // k_flush_pivot_rows + the counter reset).
+static bool reorders(const lpg_ctx *c) { return c->defer_k > 0 && c->fast_pivot && !has_comm(c) && c->colmap; }
+
 static int flush_launch(lpg_ctx *c) {
     int rc;
     if (c->timing && ((rc = timing_mark(c, 0)) || (rc = timing_mark(c, 1)))) return rc;
+    const bool re = reorders(c);
+    if (re && launch_swap_plan(lau(c), c->st, c->kq, c->lv, c->colmap, c->inv, c->pairs))
+        return fail(c, LPG_ERR_DEVICE, "swap plan launch failed");
     if (launch_flush(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, c->skip, c->flush_variant))
         return fail(c, LPG_ERR_DEVICE, "flush launch failed");
+    if (re) {
+        if (launch_swap_cols(lau(c), geo(c), c->pairs)) return fail(c, LPG_ERR_DEVICE, "swap launch failed");
+        c->permuted = true;
+    }
     c->pend = 0;
     return c->timing ? timing_mark(c, 2, 2) : 0;
 }
@@ -248,6 +266,29 @@ static int flush_launch(lpg_ctx *c) {
 static int materialize(lpg_ctx *c) {
     if (c->defer_k == 0 || c->pend == 0) return 0;
     return flush_launch(c);
+}
+
+// Up to date AND in the caller's column order (every entry point other than
+// the pivot loop itself: host reads and writes, generic kernels).
+static int canonicalize(lpg_ctx *c) {
+    int rc = materialize(c);
+    if (rc || !c->permuted) return rc;
+    const int64_t rows = c->nloc + c->nobj;
+    if (!c->tmp) {
+        c->tmp_rows = std::min<int64_t>(rows, 512);
+        HIPCHK(c, hipMalloc(&c->tmp, (size_t)c->tmp_rows * c->ld * sizeof(double)));
+    }
+    const Geo g = geo(c);
+    for (int64_t i0 = 0; i0 < rows; i0 += c->tmp_rows) {
+        const int64_t nr = std::min(c->tmp_rows, rows - i0);
+        if (launch_gather_rows(lau(c), g, c->inv, c->tmp, i0, nr)) return fail(c, LPG_ERR_DEVICE, "gather launch failed");
+        HIPCHK(c, hipMemcpy2DAsync(c->T + i0 * c->ld, c->ld * sizeof(double), c->tmp, c->ld * sizeof(double),
+                                   c->ncols * sizeof(double), nr, hipMemcpyDeviceToDevice, c->stream));
+    }
+    if (launch_iota(lau(c), c->colmap, c->ld) || launch_iota(lau(c), c->inv, c->ld))
+        return fail(c, LPG_ERR_DEVICE, "iota launch failed");
+    c->permuted = false;
+    return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -268,7 +309,7 @@ static int clear_candidates(lpg_ctx *c) {
 }
 
 static int bootstrap(lpg_ctx *c, int rule) {
-    int rc = materialize(c);
+    int rc = canonicalize(c);
     if (rc || (rc = clear_candidates(c))) return rc;
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
     const Geo g = geo(c);
@@ -287,7 +328,7 @@ static int bootstrap(lpg_ctx *c, int rule) {
 // Bootstrap onto a caller-chosen pivot (k, r): no pricing, the ratio test
 // admits only row r (either sign, |T[r][k]| > eps_piv).
 static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
-    int rc = materialize(c);
+    int rc = canonicalize(c);
     if (rc || (rc = clear_candidates(c))) return rc;
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
     if (launch_select(lau(c), geo(c), rule, true, c->st, 0, 0, c->P, c->C[1], c->C[0], c->pp, c->npp, c->basis,
@@ -595,6 +636,11 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         ALLOC(c->Cbuf, (size_t)slots * c->cs * sizeof(double));
         ALLOC(c->rq, (size_t)slots * sizeof(int64_t));
         ALLOC(c->zrow, (size_t)c->ld * sizeof(double));
+        ALLOC(c->kq, (size_t)slots * sizeof(int64_t));
+        ALLOC(c->lv, (size_t)slots * sizeof(int64_t));
+        ALLOC(c->colmap, (size_t)c->ld * sizeof(int32_t));
+        ALLOC(c->inv, (size_t)c->ld * sizeof(int32_t));
+        ALLOC(c->pairs, (size_t)(1 + 2 * 64) * sizeof(int32_t));
     }
 #undef ALLOC
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -608,7 +654,8 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         hipMemset(c->P, 0, (size_t)c->ld * sizeof(double)) != hipSuccess ||
         hipMemset(c->basis, 0, (size_t)m * sizeof(int64_t)) != hipSuccess ||
         (c->Cbuf && hipMemset(c->Cbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->cs * sizeof(double)) != hipSuccess) ||
-        (c->zrow && hipMemset(c->zrow, 0, (size_t)c->ld * sizeof(double)) != hipSuccess)) {
+        (c->zrow && hipMemset(c->zrow, 0, (size_t)c->ld * sizeof(double)) != hipSuccess) ||
+        (c->colmap && (launch_iota(lau(c), c->colmap, c->ld) || launch_iota(lau(c), c->inv, c->ld)))) {
         fail(c, LPG_ERR_DEVICE, "hipMemset failed");
         lpg_destroy(c);
         return LPG_ERR_DEVICE;
@@ -638,7 +685,7 @@ int lpg_comm_init_rccl(lpg_ctx *c, const void *uid, size_t len) {
     if (!c || !uid || len < sizeof(ncclUniqueId)) return fail(c, LPG_ERR_ARG, "bad uid");
     if (c->nccl || c->have_hops) return fail(c, LPG_ERR_STATE, "communicator already attached");
     int rc;
-    if ((rc = use_device(c))) return rc;
+    if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;   // the generic kernels work in caller order
     ncclUniqueId id;
     memcpy(&id, uid, sizeof id);
     ncclResult_t r = ncclCommInitRank(&c->nccl, c->world, id, c->rank);
@@ -652,6 +699,8 @@ int lpg_comm_init_rccl(lpg_ctx *c, const void *uid, size_t len) {
 int lpg_comm_init_host(lpg_ctx *c, const lpg_host_comm_ops *ops) {
     if (!c || !ops || !ops->allgather || !ops->allreduce_sum_f64) return fail(c, LPG_ERR_ARG, "bad host comm ops");
     if (c->nccl || c->have_hops) return fail(c, LPG_ERR_STATE, "communicator already attached");
+    int rc;
+    if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;
     c->hops = *ops;
     c->have_hops = true;
     return 0;
@@ -666,7 +715,7 @@ void lpg_destroy(lpg_ctx *c) {
     for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
-                    c->Pbuf, c->Cbuf, c->rq, c->zrow};
+                    c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->tmp};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -694,7 +743,7 @@ int lpg_load_rows(lpg_ctx *c, int64_t row0, int64_t nrows, const double *rows, i
     if (!c || !rows || row0 < 0 || nrows < 0 || row0 + nrows > c->m + c->nobj || ld < c->ncols)
         return fail(c, LPG_ERR_ARG, "lpg_load_rows: bad arguments");
     int rc;
-    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
+    if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;
     // constraint rows inside this rank's block
     const int64_t a = std::max(row0, c->row0), b = std::min(row0 + nrows, c->row0 + c->nloc);
     if (a < b)
@@ -715,7 +764,7 @@ int lpg_set_basis(lpg_ctx *c, const int64_t *basis) {
     for (int64_t i = 0; i < c->m; i++)
         if (basis[i] < 1 || basis[i] >= c->ncols) return fail(c, LPG_ERR_ARG, "basis[%lld] out of range", (long long)i);
     int rc;
-    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
+    if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(c->basis, basis, c->m * sizeof(int64_t), hipMemcpyHostToDevice));
     return reset_state(c);
@@ -736,7 +785,7 @@ int lpg_set_objective_m(lpg_ctx *c, const double *costM) {
 
 static int set_objective_row(lpg_ctx *c, const double *cost, int64_t orow) {
     int rc;
-    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
+    if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     std::vector<int64_t> hb(c->m);
     HIPCHK(c, hipMemcpy(hb.data(), c->basis, c->m * sizeof(int64_t), hipMemcpyDeviceToHost));
@@ -790,6 +839,10 @@ int lpg_generate(lpg_ctx *c, int64_t n, uint64_t seed, int kind) {
         return fail(c, LPG_ERR_ARG, "lpg_generate: need ncols == n + m + 1 and a known kind");
     int rc;
     if ((rc = use_device(c))) return rc;
+    if (c->colmap && (launch_iota(lau(c), c->colmap, c->ld) || launch_iota(lau(c), c->inv, c->ld)))
+        return fail(c, LPG_ERR_DEVICE, "iota launch failed");
+    c->permuted = false;
+    c->pend = 0;                 // the generator overwrites the whole tableau: nothing pending survives
     if (launch_generate(lau(c), geo(c), n, seed, kind, c->basis)) return fail(c, LPG_ERR_DEVICE, "generate launch failed");
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return reset_state(c);
@@ -967,7 +1020,7 @@ int lpg_solve_dual(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
     if (!c || max_pivots < 0) return fail(c, LPG_ERR_ARG, "lpg_solve_dual: bad arguments");
     if (c->world != 1 || has_comm(c)) return fail(c, LPG_ERR_STATE, "lpg_solve_dual: single rank only");
     int rc;
-    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
+    if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;
     // the dual simplex starts from a dual-feasible basis: every d_j >= -eps
     std::vector<double> obj(c->ncols);
     if ((rc = lpg_get_rows(c, c->m + c->nobj - 1, 1, obj.data(), c->ncols))) return rc;
@@ -1021,7 +1074,7 @@ int lpg_get_rows(lpg_ctx *c, int64_t row0, int64_t nrows, double *out, int64_t l
     if (!c || !out || row0 < 0 || nrows < 0 || row0 + nrows > c->m + c->nobj || ld < c->ncols)
         return fail(c, LPG_ERR_ARG, "lpg_get_rows: bad arguments");
     int rc;
-    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
+    if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const int64_t a = std::max(row0, c->row0), b = std::min(row0 + nrows, c->row0 + c->nloc);
     if (a < b)

@@ -61,6 +61,8 @@ struct Defer {
     int64_t *rq;              // K: local pivot row of pivot q, -1 on a non-owner rank
     int64_t *basis, *logk, *logr;   // bookkeeping done by prep_t in deferred mode
     const double *zrow;       // ld zeros (the padding slots of the prefetching pivot kernels)
+    int64_t *kq, *lv;         // K: entering / leaving variable of pending pivot q (logical; k_swap_plan)
+    const int32_t *colmap;    // ld: logical column held by physical column p (k_prep_d's pricing keys)
     int      q;               // pending index of this pivot
     int      on;
 };
@@ -127,6 +129,20 @@ int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s,
 // Apply the pending pivots (st->npend <= kmax) to constraint rows 0..nloc-1.
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant);
 int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0: k too large)
+// Basis-partitioned column order (single-rank deferred path): after a block,
+// every column that went nonbasic -> basic during it swaps its physical
+// position with one that went basic -> nonbasic, so the nonbasic columns keep
+// the physical positions the nonbasic columns had at the start of the solve
+// (for the synthetic LPs: one contiguous block) and a flush never meets
+// scattered live columns. launch_swap_plan (before the flush: reads npend)
+// pairs them and updates colmap / inv; launch_swap_cols (after) moves the data.
+int launch_swap_plan(const Launch &L, const DevState *st, const int64_t *kq, const int64_t *lv, int32_t *colmap,
+                     int32_t *inv, int32_t *pairs);
+int launch_swap_cols(const Launch &L, const Geo &g, const int32_t *pairs);
+// Canonical order again: rows [i0, i0 + nr) gathered through inv into tmp
+// (nr x ld), then copied back; launch_iota resets colmap / inv.
+int launch_gather_rows(const Launch &L, const Geo &g, const int32_t *inv, double *tmp, int64_t i0, int64_t nr);
+int launch_iota(const Launch &L, int32_t *a, int64_t n);
 int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
                   int64_t *basis, int64_t *logk, int64_t *logr, int variant, int skip);
 

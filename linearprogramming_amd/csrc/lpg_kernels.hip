@@ -59,7 +59,7 @@ __device__ __forceinline__ PricePart shfl_xor_pp(const PricePart &p, int mask) {
     o.v = __shfl_xor(p.v, mask, 64);
     o.j = __shfl_xor((long long)p.j, mask, 64);
     o.cls = __shfl_xor(p.cls, mask, 64);
-    o.pad = 0;
+    o.pad = __shfl_xor(p.pad, mask, 64);
     return o;
 }
 
@@ -215,6 +215,7 @@ __device__ PricePart block_argmin_pp(const PricePart &p) {
         o.j = (int64_t)l;
         o.v = __longlong_as_double((long long)rdl64((uint64_t)__double_as_longlong(p.v), src));
         o.cls = (int32_t)rdl32((uint32_t)p.cls, src);
+        o.pad = (int32_t)rdl32((uint32_t)p.pad, src);
     }
     if (NW == 1) return o;
     __shared__ PricePart sw[NW];
@@ -232,12 +233,16 @@ __device__ PricePart block_argmin_pp(const PricePart &p) {
 // Pricing candidate of column j: dR is the (real)
 // objective row entry; with Big-M (g.nobj == 2) dM is the M-part entry and the
 // comparison is lexicographic (M part first). NaN entries are never eligible.
+// j is the column's logical index (the tie-break key and what the log and
+// basis record), p its physical column in T (== j unless the single-rank
+// deferred path has reordered columns, see k_swap_plan).
 template <int RULE>
-__device__ __forceinline__ void price_one(PricePart &best, double dM, double dR, int64_t j, const Geo &g) {
+__device__ __forceinline__ void price_one(PricePart &best, double dM, double dR, int64_t j, const Geo &g,
+                                          int64_t p = -1) {
     if (j < 1 || j > g.nact) return;
     PricePart c;
     c.j = j;
-    c.pad = 0;
+    c.pad = (int32_t)(p < 0 ? j : p);
     if (g.nobj == 1) {
         if (!(dR < -g.eps_opt)) return;
         c.cls = 0;
@@ -849,6 +854,7 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
     for (int u = 0; u < kPF; u++)
         pq[u] = *(const d2 *)((u < npf ? D.Pbuf + (int64_t)u * g.ld : D.zrow) + jc);
     const int64_t rqv = lane < D.q ? D.rq[lane] : -1;   // lane q of every wave holds r_q
+    const int2 lj = col ? ((const int2 *)D.colmap)[j2] : int2{0, 0};   // logical indices of the two columns
     if (status != RUNNING) return;
     LPG_PH(0, 1);
     best = block_argmin_cand<NT / 64>(best);
@@ -866,6 +872,8 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
         st->slot[s].r = best.row;
         D.rq[D.q] = rl;
         st->npend = D.q + 1;
+        D.kq[D.q] = k;                       // entering and leaving variables of the block (k_swap_plan)
+        D.lv[D.q] = D.basis[best.row];
         D.basis[best.row] = k;
         const int64_t n = st->pivots;
         if (D.logk && n < st->logcap) {
@@ -932,8 +940,8 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
         dR.y = fma(cR, p.y, dR.y);
         *(d2 *)(T + rR * g.ld + 2 * j2) = dR;
         if (g.nobj == 2) *(d2 *)(T + rM * g.ld + 2 * j2) = dM;
-        price_one<RULE>(pbest, dM.x, dR.x, 2 * j2, g);
-        price_one<RULE>(pbest, dM.y, dR.y, 2 * j2 + 1, g);
+        price_one<RULE>(pbest, dM.x, dR.x, lj.x, g, 2 * j2);
+        price_one<RULE>(pbest, dM.y, dR.y, lj.y, g, 2 * j2 + 1);
     }
     LPG_PH(0, 4);
     pbest = block_argmin_pp<RULE, NT / 64>(pbest);
@@ -999,15 +1007,15 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
         }
         return;
     }
-    const int64_t kn = pb.j;
+    const int64_t kn = pb.j, kp = pb.pad;   // logical (log, basis, slot) and physical (loads) column
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         dst->status = RUNNING;
         dst->k = kn;
     }
     // ---- round 2: column k_{t+1} as stored and P_q[k_{t+1}] (lane q)
     double oa = 0.0;
-    if (row) oa = T[i * g.ld + kn];
-    const double pkl = lq ? D.Pbuf[(int64_t)lane * g.ld + kn] : 0.0;
+    if (row) oa = T[i * g.ld + kp];
+    const double pkl = lq ? D.Pbuf[(int64_t)lane * g.ld + kp] : 0.0;
     LPG_PH(1, 3);
     const uint64_t p0b = (uint64_t)__double_as_longlong(p0l), pkb = (uint64_t)__double_as_longlong(pkl);
     Cand best{0.0, 0.0, 0, -1};
@@ -2086,13 +2094,153 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
     if (q >= np) return;
     const int64_t r = rq[q];
     if (r < 0) return;                                  // pivot row on another rank
-    for (int q2 = q + 1; q2 < np; q2++)
-        if (rq[q2] == r) return;                        // a later pivot replaces this row again
+    const int lane = threadIdx.x & 63;
+    // lane u holds r_u and the multiplier -C_u[r] of a later pivot u (-0 elsewhere)
+    const int64_t ru = lane < np ? rq[lane] : -1;
+    if (__ballot(lane > q && ru == r)) return;          // a later pivot replaces this row again
+    const double cl = (lane > q && lane < np) ? -Cbuf[(int64_t)lane * cs + r] : -0.0;
+    const uint64_t clb = (uint64_t)__double_as_longlong(cl);
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= g.ncols) return;
-    double x = Pbuf[(int64_t)q * g.ld + j];
-    for (int q2 = q + 1; q2 < np; q2++) x = fma(-Cbuf[(int64_t)q2 * cs + r], Pbuf[(int64_t)q2 * g.ld + j], x);
-    T[r * g.ld + j] = x;
+    const bool ok = j < g.ncols;
+    double x = ok ? Pbuf[(int64_t)q * g.ld + j] : 0.0;
+    for (int q0 = q + 1; q0 < np; q0 += 16) {          // 16 pivots' loads in flight at once
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = (ok && q0 + u < np) ? Pbuf[(int64_t)(q0 + u) * g.ld + j] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            if (q0 + u < np) x = fma(__longlong_as_double((long long)rdl64(clb, q0 + u)), v[u], x);
+    }
+    if (ok) T[r * g.ld + j] = x;
+}
+
+// ------------------------------------------------------------------------
+// Basis-partitioned column order (lpg_internal.h). Events of the block: pivot
+// q enters kq[q] and lets lv[q] leave. A column whose first and last events
+// are both "enter" went nonbasic -> basic (set E), both "leave": basic ->
+// nonbasic (set L); |E| == |L|. The i-th of E (in event order) trades
+// physical positions with the i-th of L. One wave; pairs[0] = count, then
+// (a, b) physical pairs.
+// ------------------------------------------------------------------------
+
+__global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ st, const int64_t *__restrict__ kq,
+                                                  const int64_t *__restrict__ lv, int32_t *__restrict__ colmap,
+                                                  int32_t *__restrict__ inv, int32_t *__restrict__ pairs) {
+    const int np = (int)st->npend;
+    const int q = threadIdx.x;
+    const int64_t x = q < np ? kq[q] : -1, y = q < np ? lv[q] : -1;
+    __shared__ int64_t sk[64], sl[64];
+    sk[q] = x;
+    sl[q] = y;
+    __syncthreads();
+    // x (entering at q) is in E iff no later event touches x and its first event is an entry
+    bool inE = q < np, inL = q < np;
+    int fx = q, fy = q;           // first event index of x / y, and its kind
+    bool fxe = true, fye = false;
+    for (int u = 0; u < np; u++) {
+        const int64_t a = sk[u], b = sl[u];
+        if (u > q) {
+            if (a == x || b == x) inE = false;
+            if (a == y || b == y) inL = false;
+        } else if (u < q) {
+            if (a == x && u < fx) { fx = u; fxe = true; }
+            if (b == x && u < fx) { fx = u; fxe = false; }
+            if (a == y && u < fy) { fy = u; fye = true; }
+            if (b == y && u < fy) { fy = u; fye = false; }
+        }
+    }
+    inE = inE && fxe;
+    inL = inL && !fye;
+    const unsigned long long me = __ballot(inE), ml = __ballot(inL);
+    const unsigned long long below = (q == 0) ? 0ull : (~0ull >> (64 - q));
+    const int ie = __popcll(me & below), il = __popcll(ml & below);
+    __shared__ int64_t eE[64], eL[64];
+    if (inE) eE[ie] = x;
+    if (inL) eL[il] = y;
+    __syncthreads();
+    const int n = __popcll(me);   // == __popcll(ml)
+    if (q < n) {
+        const int64_t ce = eE[q], cl = eL[q];
+        const int32_t a = inv[ce], b = inv[cl];
+        pairs[1 + 2 * q] = a;
+        pairs[2 + 2 * q] = b;
+        colmap[a] = (int32_t)cl;
+        colmap[b] = (int32_t)ce;
+        inv[cl] = a;
+        inv[ce] = b;
+    }
+    if (q == 0) pairs[0] = n;
+}
+
+// one thread per row (constraint and objective rows) and group of 16 pairs
+// (blockIdx.y): swap the planned pairs
+__global__ __launch_bounds__(kBlock) void k_swap_cols(double *__restrict__ T, Geo g, const int32_t *__restrict__ pairs) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int n = pairs[0];
+    if (i >= g.nloc + g.nobj || n == 0) return;
+    double *row = T + i * g.ld;
+    for (int p0 = 16 * blockIdx.y; p0 < n; p0 += 16 * gridDim.y) {      // 16 pairs' loads in flight at once
+        double va[16], vb[16];
+        int ia[16], ib[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            ia[u] = p0 + u < n ? pairs[1 + 2 * (p0 + u)] : 0;
+            ib[u] = p0 + u < n ? pairs[2 + 2 * (p0 + u)] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            va[u] = row[ia[u]];
+            vb[u] = row[ib[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            if (p0 + u < n) {
+                row[ia[u]] = vb[u];
+                row[ib[u]] = va[u];
+            }
+    }
+}
+
+int launch_swap_plan(const Launch &L, const DevState *st, const int64_t *kq, const int64_t *lv, int32_t *colmap,
+                     int32_t *inv, int32_t *pairs) {
+    hipLaunchKernelGGL(k_swap_plan, dim3(1), dim3(64), 0, (hipStream_t)L.stream, st, kq, lv, colmap, inv, pairs);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_swap_cols(const Launch &L, const Geo &g, const int32_t *pairs) {
+    const int64_t rows = g.nloc + g.nobj;
+    hipLaunchKernelGGL(k_swap_cols, dim3((unsigned)((rows + kBlock - 1) / kBlock), 4), dim3(kBlock), 0,
+                       (hipStream_t)L.stream, g.T, g, pairs);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// tmp[r][j] = T[i0 + r][inv[j]], j < ncols (column 0 and the padding map to themselves)
+__global__ __launch_bounds__(kBlock) void k_gather_rows(const double *__restrict__ T, Geo g,
+                                                        const int32_t *__restrict__ inv, double *__restrict__ tmp,
+                                                        int64_t i0, int64_t nr) {
+    const int64_t r = blockIdx.y;
+    if (r >= nr) return;
+    const double *src = T + (i0 + r) * g.ld;
+    double *dst = tmp + r * g.ld;
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < g.ncols; j += (int64_t)gridDim.x * kBlock)
+        dst[j] = src[inv[j]];
+}
+
+int launch_gather_rows(const Launch &L, const Geo &g, const int32_t *inv, double *tmp, int64_t i0, int64_t nr) {
+    const int64_t tiles = std::min<int64_t>((g.ncols + kBlock - 1) / kBlock, 64);
+    hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)tiles, (unsigned)nr), dim3(kBlock), 0, (hipStream_t)L.stream,
+                       g.T, g, inv, tmp, i0, nr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+__global__ void k_iota(int32_t *a, int64_t n) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+        a[j] = (int32_t)j;
+}
+
+int launch_iota(const Launch &L, int32_t *a, int64_t n) {
+    hipLaunchKernelGGL(k_iota, dim3(256), dim3(kBlock), 0, (hipStream_t)L.stream, a, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 struct FlushCfg {
