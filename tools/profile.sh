@@ -8,7 +8,7 @@ set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 CFG=${CFG:-3}
-STEPS=${STEPS:-64}   # whole deferred blocks (2 x 32), no warm-up: every k_flushm launch applies 32 pivots
+STEPS=${STEPS:-128}  # whole deferred blocks (2 x 64), no warm-up: every flush applies a full block
 mkdir -p $OUT
 echo "[profile] trace" >&2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
