@@ -96,6 +96,7 @@ struct lpg_ctx {
     hipGraphExec_t graph[2] = {nullptr, nullptr};   // by parity of the first pivot
     int graph_rule[2] = {-1, -1};
     bool use_graphs = true;
+    bool graph_comm = true;       // RCCL collectives captured into the replayed graphs (cleared if capture fails)
     // timing
     bool timing = false;
     TimingRing tr;
@@ -295,9 +296,13 @@ static int canonicalize(lpg_ctx *c) {
 // pivot loop
 // ---------------------------------------------------------------------------
 
+// Ratio candidates per rank: the deferred prefetching pair (single rank or
+// not) works with nsel_d, the generic kernels with nsel.
+static int cand_per_rank(const lpg_ctx *c) { return (c->defer_k > 0 && c->fast_pivot) ? c->nsel_d : c->nsel; }
+
 static int exchange_candidates(lpg_ctx *c) {
     if (!has_comm(c)) return 0;
-    return comm_allgather(c, c->part, c->cand, sizeof(Cand) * (size_t)c->nsel);
+    return comm_allgather(c, c->part, c->cand, sizeof(Cand) * (size_t)cand_per_rank(c));
 }
 
 // The generic select of a bootstrap writes nsel ratio candidates, and the
@@ -400,7 +405,9 @@ static int enqueue(lpg_ctx *c, int64_t npiv, int rule) {
     // eager-mode timing brackets every update, which a graph cannot; deferred
     // timing brackets only the flushes, which stay outside the graph
     const bool timed = c->timing && c->defer_k == 0;
-    if (!c->use_graphs || timed || has_comm(c) || npiv < 2 * G || (G & 1)) return enqueue_eager(c, npiv, rule);
+    // a host-callback communicator cannot be captured; RCCL's collectives can
+    const bool comm_ok = !has_comm(c) || (c->nccl && !c->have_hops && c->graph_comm);
+    if (!c->use_graphs || timed || !comm_ok || npiv < 2 * G || (G & 1)) return enqueue_eager(c, npiv, rule);
     int rc;
     if (c->pend) {                           // finish the open block first
         const int64_t a = G - c->pend;
@@ -408,8 +415,14 @@ static int enqueue(lpg_ctx *c, int64_t npiv, int rule) {
         npiv -= a;
     }
     const int par = c->par;                  // G is even: every block starts at this parity
-    if (npiv >= G && (!c->graph[par] || c->graph_rule[par] != rule))
-        if ((rc = graph_build(c, rule))) return rc;
+    if (npiv >= G && (!c->graph[par] || c->graph_rule[par] != rule)) {
+        if ((rc = graph_build(c, rule))) {
+            if (!has_comm(c)) return rc;
+            c->graph_comm = false;           // this RCCL build does not capture: launch eagerly from now on
+            c->err[0] = 0;
+            return enqueue_eager(c, npiv, rule);
+        }
+    }
     for (; npiv >= G; npiv -= G) {
         HIPCHK(c, hipGraphLaunch(c->graph[par], c->stream));
         c->enq += G;
@@ -428,6 +441,7 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
     // one (any world size) P must be exchanged first.
     const bool fuse = !has_comm(c);
     const int ncand = c->nsel * c->world;
+    const int ncand_d = c->nsel_d * c->world;
     for (int64_t q = 0; q < npiv; q++) {
         const int s = c->par, s1 = s ^ 1;
         const Defer D = defer_of(c, c->pend);
@@ -439,6 +453,24 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
             if (launch_pivot_d(L, g, rule, c->st, s, s1, c->part, c->nsel_d, P, c->C[s], c->C[s1], c->pp, c->npp_d,
                                c->basis, D, c->pivot_nt))
                 return fail(c, LPG_ERR_DEVICE, "pivot launch failed");
+            if (++c->pend == c->defer_k && !c->capture_block)
+                if ((rc = flush_launch(c))) return rc;
+            c->par = s1;
+            c->enq++;
+            continue;
+        }
+        if (D.on && c->fast_pivot) {            // deferred, with a communicator: prefetching prep, exchange, generic select
+            // (k_select_d under a communicator diverged from the oracle after a few pivots in the 2-rank
+            // test; the generic k_select is bitwise right there and is used instead)
+            if (launch_prep_dm(L, g, rule, c->st, s, c->cand, ncand_d, P, c->C[s], c->npp_d, D))
+                return fail(c, LPG_ERR_DEVICE, "prep launch failed");
+            if ((rc = comm_allreduce_sum(c, P, (size_t)c->ld))) return rc;
+            if (launch_price(L, g, rule, 1, c->st, s, P, c->C[s], c->pp, c->pc, c->npp, true))
+                return fail(c, LPG_ERR_DEVICE, "price launch failed");
+            if (launch_select(L, g, rule, false, c->st, s, s1, P, c->C[s], c->C[s1], c->pp, c->npp, c->basis, c->part,
+                              c->nsel_d, 0, -1, c->pc, c->skip, D))
+                return fail(c, LPG_ERR_DEVICE, "select launch failed");
+            if ((rc = exchange_candidates(c))) return rc;
             if (++c->pend == c->defer_k && !c->capture_block)
                 if ((rc = flush_launch(c))) return rc;
             c->par = s1;
@@ -600,10 +632,11 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     const int64_t maxloc = (m + world - 1) / world + c->nobj;   // identical on every rank
     c->nsel = (int)std::min<int64_t>((maxloc + kBlock - 1) / kBlock, kMaxSelBlocks);
     const char *pn = getenv("LPG_PIVOT_NT");
-    if (pn) c->pivot_nt = atoi(pn) == 128 ? 128 : 256;
+    if (pn && world == 1) c->pivot_nt = atoi(pn) == 128 ? 128 : 256;
     c->npp_d = pivot_d_blocks(g, 0, c->pivot_nt);
-    c->nsel_d = pivot_d_blocks(g, 1, c->pivot_nt);              // k_select_d: one row per thread
-    if (world > 1) c->fast_pivot = false;
+    // k_select_d: one row per thread; with world > 1 the count must be the
+    // same on every rank (the candidates are allgathered)
+    c->nsel_d = world == 1 ? pivot_d_blocks(g, 1, c->pivot_nt) : (int)((maxloc + 255) / 256);
 #define ALLOC(p, bytes)                                                                    \
     do {                                                                                   \
         hipError_t e_ = hipMalloc((void **)&(p), (bytes));                                 \
@@ -624,7 +657,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     ALLOC(c->pp, (size_t)std::max(c->npp, c->npp_d) * sizeof(PricePart));
     ALLOC(c->pc, (size_t)c->npp * sizeof(int));
     ALLOC(c->part, (size_t)std::max(c->nsel, c->nsel_d) * sizeof(Cand));
-    if (world > 1) ALLOC(c->cand, (size_t)c->nsel * world * sizeof(Cand));
+    if (world > 1) ALLOC(c->cand, (size_t)std::max(c->nsel, c->nsel_d) * world * sizeof(Cand));
     else c->cand = c->part;
     ALLOC(c->basis, (size_t)m * sizeof(int64_t));
     ALLOC(c->st, sizeof(DevState));
@@ -681,6 +714,17 @@ int lpg_comm_unique_id(void *uid, size_t len) {
     return 0;
 }
 
+// With a communicator the deferred pair runs in 256-thread blocks (its
+// candidate count must match across ranks): drop a 128-thread choice.
+static void comm_pivot_blocks(lpg_ctx *c) {
+    if (c->pivot_nt == 256) return;
+    c->pivot_nt = 256;
+    c->npp_d = pivot_d_blocks(geo(c), 0, 256);    // buffers were sized for the larger 128-thread counts
+    c->nsel_d = pivot_d_blocks(geo(c), 1, 256);
+    c->booted = false;
+    graph_drop(c);
+}
+
 int lpg_comm_init_rccl(lpg_ctx *c, const void *uid, size_t len) {
     if (!c || !uid || len < sizeof(ncclUniqueId)) return fail(c, LPG_ERR_ARG, "bad uid");
     if (c->nccl || c->have_hops) return fail(c, LPG_ERR_STATE, "communicator already attached");
@@ -688,6 +732,7 @@ int lpg_comm_init_rccl(lpg_ctx *c, const void *uid, size_t len) {
     if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;   // the generic kernels work in caller order
     ncclUniqueId id;
     memcpy(&id, uid, sizeof id);
+    comm_pivot_blocks(c);
     ncclResult_t r = ncclCommInitRank(&c->nccl, c->world, id, c->rank);
     if (r != ncclSuccess) {
         c->nccl = nullptr;
@@ -701,6 +746,7 @@ int lpg_comm_init_host(lpg_ctx *c, const lpg_host_comm_ops *ops) {
     if (c->nccl || c->have_hops) return fail(c, LPG_ERR_STATE, "communicator already attached");
     int rc;
     if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;
+    comm_pivot_blocks(c);
     c->hops = *ops;
     c->have_hops = true;
     return 0;

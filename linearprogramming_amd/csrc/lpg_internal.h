@@ -126,6 +126,13 @@ int pivot_d_blocks(const Geo &g, int which, int nt);
 int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, Cand *part, int nsel,
                    double *P, const double *Cs, double *Cs1, PricePart *pp, int npp, const int64_t *basis,
                    const Defer &D, int nt);
+// The same pair with a communicator: launch_prep_dm, then the caller's
+// allreduce of P and launch_price(mode 1), then launch_select_dm.
+int launch_prep_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s, const Cand *cand, int ncand,
+                   double *P, const double *Cs, int npp_d, const Defer &D);
+int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, const double *Cs,
+                     double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part, int nsel,
+                     const Defer &D);
 // Apply the pending pivots (st->npend <= kmax) to constraint rows 0..nloc-1.
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant);
 int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0: k too large)

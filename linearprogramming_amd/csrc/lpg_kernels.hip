@@ -820,7 +820,11 @@ __device__ unsigned long long g_ph[2][16];
 #define LPG_PH(kern, k) do { } while (0)
 #endif
 
-template <int RULE, int kPF, int NT>
+// MR (multi-rank): the pivot row lives on one rank; the owner computes P,
+// every other rank writes -0 (the identity of the allreduce that follows, so
+// the sum is the owner's row bit for bit, signed zeros included), and the
+// pricing runs after the exchange (k_price), not here.
+template <int RULE, int kPF, int NT, bool MR>
 __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, DevState *st, int s,
                                                    const Cand *__restrict__ cand, int ncand, double *__restrict__ P,
                                                    const double *__restrict__ Cs, PricePart *__restrict__ pp, Defer D) {
@@ -866,7 +870,8 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
         }
         return;
     }
-    const int64_t rl = best.row - g.row0;   // single rank: always local
+    const bool own = !MR || (best.row >= g.row0 && best.row < g.row0 + g.nloc);   // uniform
+    const int64_t rl = own ? best.row - g.row0 : -1;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const int64_t k = st->slot[s].k;
         st->slot[s].r = best.row;
@@ -889,9 +894,9 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
     // this row (x = P_qs), found by a ballot, so each step is one fma with
     // the multiplier read back from lane q (v_readlane: no LDS, no barrier)
     d2 t = d2{0.0, 0.0};
-    if (col) t = *(const d2 *)(T + rl * g.ld + 2 * j2);
-    const double cl = lane < D.q ? -D.Cbuf[(int64_t)lane * D.cs + rl] : -0.0;
-    const unsigned long long hit = __ballot(lane < D.q && rqv == rl);
+    if (col && own) t = *(const d2 *)(T + rl * g.ld + 2 * j2);
+    const double cl = (own && lane < D.q) ? -D.Cbuf[(int64_t)lane * D.cs + rl] : -0.0;
+    const unsigned long long hit = __ballot(own && lane < D.q && rqv == rl);
     const int qs = hit ? 63 - __clzll((long long)hit) : -1;
     LPG_PH(0, 3);
     PricePart pbest{0.0, -1, 0, 0};
@@ -927,6 +932,10 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
             t.x = fma(c, v.x, t.x);
             t.y = fma(c, v.y, t.y);
         }
+    }
+    if (MR) {
+        if (col) *(d2 *)(P + 2 * j2) = own ? d2{t.x / best.piv, t.y / best.piv} : d2{-0.0, -0.0};
+        return;
     }
     if (col) {
         const double piv = best.piv;
@@ -1119,8 +1128,8 @@ int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s,
     hipStream_t stream = (hipStream_t)L.stream;
 #define LPG_PD(R, PF, NT)                                                                                             \
     do {                                                                                                              \
-        hipLaunchKernelGGL((k_prep_d<R, PF, NT>), dim3(npp), dim3(NT), 0, stream, g.T, g, st, s, part, nsel, P, Cs, pp, \
-                           D);                                                                                        \
+        hipLaunchKernelGGL((k_prep_d<R, PF, NT, false>), dim3(npp), dim3(NT), 0, stream, g.T, g, st, s, part, nsel, P, \
+                           Cs, pp, D);                                                                                \
         hipLaunchKernelGGL((k_select_d<R, PF, NT>), dim3(nsel), dim3(NT), 0, stream, g.T, g, st, s, s1, Cs, Cs1, pp,   \
                            npp, basis, part, D);                                                                      \
     } while (0)
@@ -1139,6 +1148,49 @@ int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s,
     }
 #undef LPG_PD_NT
 #undef LPG_PD
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Multi-rank deferred pivot, first half: k_prep_d<MR> over npp_d column
+// blocks reading ncand gathered candidates (P: owner's row, -0 elsewhere).
+int launch_prep_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s, const Cand *cand, int ncand,
+                   double *P, const double *Cs, int npp_d, const Defer &D) {
+    if (npp_d != pivot_d_blocks(g, 0, 256)) return -1;
+    hipStream_t stream = (hipStream_t)L.stream;
+#define LPG_PM(R, PF)                                                                                                 \
+    hipLaunchKernelGGL((k_prep_d<R, PF, 256, true>), dim3(npp_d), dim3(256), 0, stream, g.T, g, st, s, cand, ncand, P, \
+                       Cs, nullptr, D)
+    const bool wide = D.q >= 32;
+    if (rule == RULE_BLAND) {
+        if (wide) LPG_PM(RULE_BLAND, 64);
+        else LPG_PM(RULE_BLAND, 32);
+    } else {
+        if (wide) LPG_PM(RULE_DANTZIG, 64);
+        else LPG_PM(RULE_DANTZIG, 32);
+    }
+#undef LPG_PM
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ... second half, after the pivot-row exchange and k_price: k_select_d over
+// nsel blocks (>= the local rows + objective rows), npp pricing partials.
+int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, const double *Cs,
+                     double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part, int nsel,
+                     const Defer &D) {
+    if ((int64_t)nsel * 256 < g.nloc + g.nobj) return -1;
+    hipStream_t stream = (hipStream_t)L.stream;
+#define LPG_SM(R, PF)                                                                                               \
+    hipLaunchKernelGGL((k_select_d<R, PF, 256>), dim3(nsel), dim3(256), 0, stream, g.T, g, st, s, s1, Cs, Cs1, pp, \
+                       npp, basis, part, D)
+    const bool wide = D.q >= 32;
+    if (rule == RULE_BLAND) {
+        if (wide) LPG_SM(RULE_BLAND, 64);
+        else LPG_SM(RULE_BLAND, 32);
+    } else {
+        if (wide) LPG_SM(RULE_DANTZIG, 64);
+        else LPG_SM(RULE_DANTZIG, 32);
+    }
+#undef LPG_SM
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -6,7 +6,10 @@ the reference turns ``valid == 0`` into an ``ERROR: ...`` line.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import os
+import sys
 from dataclasses import dataclass
 
 import numpy as np
@@ -34,6 +37,22 @@ class SolveResult:
 
 def _res(r: L.Result) -> SolveResult:
     return SolveResult(r.status, r.pivots, r.objective, r.entering, r.leaving, r.rule)
+
+
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """RCCL prints a version banner on the process's stdout at init; keep
+    stdout for results (bench.py's one JSON line) by pointing fd 1 at fd 2."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        ctypes.CDLL(None).fflush(None)      # C stdio buffers go out through the redirected fd
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def device_count() -> int:
@@ -88,13 +107,16 @@ class Engine:
     # -- communication ---------------------------------------------------
     def comm_init_rccl(self, uid: bytes):
         buf = ctypes.create_string_buffer(bytes(uid), len(uid))
-        self._check(self.lib.lpg_comm_init_rccl(self._ctx, buf, len(uid)), "lpg_comm_init_rccl")
+        with _stdout_to_stderr():
+            rc = self.lib.lpg_comm_init_rccl(self._ctx, buf, len(uid))
+        self._check(rc, "lpg_comm_init_rccl")
 
     @staticmethod
     def rccl_unique_id() -> bytes:
         lib = L.load()
         buf = ctypes.create_string_buffer(128)
-        rc = lib.lpg_comm_unique_id(buf, 128)
+        with _stdout_to_stderr():
+            rc = lib.lpg_comm_unique_id(buf, 128)
         if rc != 0:
             raise LPGError(f"lpg_comm_unique_id rc={rc}: {lib.lpg_last_error(None).decode()}")
         return buf.raw

@@ -1,4 +1,3 @@
 set -u
-export TMPDIR=/tmp
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pr3 -o run -- python3 bench.py --steps 512 --warmup 64 --no-cpu > gpurun_out/pr3.json 2>/dev/null || exit $?
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pr5 -o run -- python3 bench.py --config 5 --no-cpu > gpurun_out/pr5.json 2>/dev/null || exit $?
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_iter.log 2>&1 || exit $?
+timeout -k 10 200 python bench.py --no-cpu --force-rccl --steps 256 > gpurun_out/rccl1.json 2>gpurun_out/rccl1.err || exit $?
