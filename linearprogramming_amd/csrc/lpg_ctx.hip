@@ -96,7 +96,9 @@ struct lpg_ctx {
     hipGraphExec_t graph[2] = {nullptr, nullptr};   // by parity of the first pivot
     int graph_rule[2] = {-1, -1};
     bool use_graphs = true;
-    bool graph_comm = true;       // RCCL collectives captured into the replayed graphs (cleared if capture fails)
+    bool graph_comm = false;      // RCCL collectives captured into the replayed graphs (LPG_GRAPH_RCCL=1;
+                                  // cleared if capture fails). Off by default: on one GPU (1-rank
+                                  // communicator) it measured no gain, and the 8-GPU path is untested here
     // timing
     bool timing = false;
     TimingRing tr;
@@ -605,6 +607,8 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->update_variant = uv ? atoi(uv) : -1;   // -1: size-adaptive default (launch_update)
     const char *ng = getenv("LPG_NO_GRAPH");
     c->use_graphs = !(ng && atoi(ng));
+    const char *gr = getenv("LPG_GRAPH_RCCL");
+    c->graph_comm = gr && atoi(gr);
     const char *ns = getenv("LPG_NO_SKIP");
     c->skip = ((flags & LPG_FLAG_NO_SKIP) || (ns && atoi(ns))) ? 0 : 1;
     const char *dk = getenv("LPG_DEFER");

@@ -159,13 +159,15 @@ def test_two_processes_gloo_bitwise(lpg):
     assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
 
 
-@pytest.mark.parametrize("m,n,defer", [(300, 500, None), (1024, 2048, None), (1024, 2048, "64")])
-def test_rccl_single_rank_communicator(lpg, m, n, defer, monkeypatch):
+@pytest.mark.parametrize("m,n,defer,graphs", [(300, 500, None, "0"), (1024, 2048, None, "0"), (1024, 2048, "64", "0"),
+                                              (1024, 2048, None, "1")])
+def test_rccl_single_rank_communicator(lpg, m, n, defer, graphs, monkeypatch):
     """The RCCL transport on a 1-rank communicator: every per-pivot ncclAllReduce
     (pivot row) and ncclAllGather (ratio candidates) really runs, and the result
     is bitwise the engine without a communicator (and the oracle)."""
     if defer is not None:
         monkeypatch.setenv("LPG_DEFER", defer)
+    monkeypatch.setenv("LPG_GRAPH_RCCL", graphs)     # 1: the collectives are captured into the replayed graphs
     e = lpg.Engine(m, n + m + 1)
     e.comm_init_rccl(lpg.Engine.rccl_unique_id())
     e.generate(n, 41, 0)
