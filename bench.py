@@ -6,8 +6,9 @@ the device (splitmix64, seed 20220518). A "step" is one simplex pivot:
 price (argmin over the reduced-cost row) -> ratio test (min over the entering
 column) -> Gauss-Jordan rank-1 update of the whole tableau. By default the
 update is deferred: prep / select evaluate the pending chain for the entries
-they need and k_flush applies each block of K pivots (LPG_DEFER, default 32)
-to the constraint rows in one HBM pass, bitwise identical to K eager updates.
+they need and k_flushw applies each block of K pivots (LPG_DEFER; 64 for
+tableaus >= 512 MB per rank, else 32) to the constraint rows in one HBM pass,
+bitwise identical to K eager updates.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -18,11 +19,11 @@ GPU); per pivot the ranks allgather the ratio candidates and allreduce the
 pivot row over RCCL (strong scaling: the LP is the same for every N).
 
 Rank 0 prints ONE JSON line. `roofline.achieved` = algorithmic bytes of one
-launch of the dominant kernel on rank 0 (k_flush: 16 B x local constraint
+launch of the dominant kernel on rank 0 (k_flushw: 16 B x local constraint
 rows x columns not skipped, one read + one write of every entry the block
 changes; eager k_update: the same over all rows for one pivot) / its mean
-device time, timed with HIP events on the engine's own stream over the timed
-region. `cpu_baseline` =
+device time, timed with HIP events around that kernel alone on the engine's
+own stream over the timed region. `cpu_baseline` =
 the CPU oracle (oracle/liblpo.so, same pivot rules, OpenMP) on the same LP,
 rank 0 at N=1 only, for a bounded number of pivots; its pivot sequence is
 compared with the GPU's.
@@ -55,8 +56,8 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=192)   # 6 whole deferred blocks of 32
-    ap.add_argument("--warmup", type=int, default=64)   # 2 blocks: page-in + the replayed hipGraph is built
+    ap.add_argument("--steps", type=int, default=192)   # 3 whole deferred blocks of 64
+    ap.add_argument("--warmup", type=int, default=64)   # 1 block: page-in + the replayed hipGraph is built
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
@@ -117,7 +118,8 @@ def config5(a):
             "config": {"workload": cfg["name"], "m": m, "n": n, "rule": "bland", "art_first": art_first},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "lpg::k_flush" if eng.info.defer_k else "lpg::k_update",
+                         "kernel": ("lpg::k_flushw" if eng.info.defer_k > 32 else "lpg::k_flushm") if eng.info.defer_k
+                                   else "lpg::k_update",
                          "launches_timed": timing.update_count,
                          "algorithmic_bytes_per_launch": touched,
                          "full_tableau_bytes_per_launch": eng.info.bytes_per_pivot, "update_ms_mean": upd_ms},
@@ -230,7 +232,9 @@ def main():
         done = int(dd.item())
     upd_ms = timing.update_ms / max(timing.update_count, 1)
     # bytes the update / flush kernel actually read + wrote (columns whose
-    # pending P entries are all zero are not counted)
+    # pending P entries are all zero are not counted); in
+    # deferred mode the events bracket the block pass alone (k_flushw /
+    # k_flushm), so this agrees with rocprofv3's average for that kernel
     touched = timing.update_bytes / max(timing.update_count, 1)
     defer = eng.info.defer_k
     achieved = touched / (upd_ms * 1e-3) / 1e9 if upd_ms > 0 else 0.0
@@ -256,7 +260,8 @@ def main():
                    "update_variant": int(os.environ.get("LPG_UPDATE_VARIANT", "-1"))},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": (f"lpg::k_flush (Gauss-Jordan, {defer} pending pivots per pass)" if defer
+                     "kernel": (f"lpg::{'k_flushw' if defer > 32 else 'k_flushm'} (Gauss-Jordan, {defer} pending "
+                                f"pivots per pass; HIP events around this kernel alone)" if defer
                                 else "lpg::k_update (Gauss-Jordan rank-1)"),
                      "launches_timed": timing.update_count,
                      "algorithmic_bytes_per_launch": touched,

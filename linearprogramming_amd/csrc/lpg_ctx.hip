@@ -249,20 +249,26 @@ static Defer defer_of(const lpg_ctx *c, int q) {
 // k_flush_pivot_rows + the counter reset).
 static bool reorders(const lpg_ctx *c) { return c->defer_k > 0 && c->fast_pivot && !has_comm(c) && c->colmap; }
 
+// The timing ring brackets the block pass alone (k_flushw / k_flushm), the
+// kernel the roofline reports; the swap plan, pivot-row rewrite and column
+// swaps around it count as "other" time per pivot.
 static int flush_launch(lpg_ctx *c) {
     int rc;
-    if (c->timing && ((rc = timing_mark(c, 0)) || (rc = timing_mark(c, 1)))) return rc;
     const bool re = reorders(c);
     if (re && launch_swap_plan(lau(c), c->st, c->kq, c->lv, c->colmap, c->inv, c->pairs))
         return fail(c, LPG_ERR_DEVICE, "swap plan launch failed");
-    if (launch_flush(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, c->skip, c->flush_variant))
+    if (c->timing && ((rc = timing_mark(c, 0)) || (rc = timing_mark(c, 1)))) return rc;
+    if (launch_flush_main(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, c->skip, c->flush_variant))
+        return fail(c, LPG_ERR_DEVICE, "flush launch failed");
+    if (c->timing && (rc = timing_mark(c, 2, 2))) return rc;
+    if (launch_flush_tail(lau(c), geo(c), c->st, defer_of(c, 0), c->pend))
         return fail(c, LPG_ERR_DEVICE, "flush launch failed");
     if (re) {
         if (launch_swap_cols(lau(c), geo(c), c->pairs)) return fail(c, LPG_ERR_DEVICE, "swap launch failed");
         c->permuted = true;
     }
     c->pend = 0;
-    return c->timing ? timing_mark(c, 2, 2) : 0;
+    return 0;
 }
 
 // Bring the constraint rows up to date (no-op in eager mode or with nothing pending).

@@ -2346,7 +2346,24 @@ int flush_kmax_supported(int k) {
 static_assert(offsetof(DevState, fwork) == offsetof(DevState, npend) + sizeof(int64_t),
               "launch_flush clears npend and fwork with one memset");
 
+int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax) {
+    kmax = flush_kmax_supported(kmax);
+    if (!kmax) return -1;
+    hipStream_t stream = (hipStream_t)L.stream;
+    const int64_t ntiles_p = (g.ncols + kBlock - 1) / kBlock;   // k_flush_pivot_rows column tiles
+    hipLaunchKernelGGL(k_flush_pivot_rows, dim3((unsigned)ntiles_p, (unsigned)kmax), dim3(kBlock), 0, stream, g.T, g, st,
+                       D.Pbuf, D.Cbuf, D.cs, D.rq);
+    if (hipGetLastError() != hipSuccess) return -1;
+    // the pending block is applied: clear it and the dequeue head
+    return hipMemsetAsync(&st->npend, 0, sizeof(int64_t) + sizeof(unsigned long long), stream) == hipSuccess ? 0 : -1;
+}
+
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant) {
+    int rc = launch_flush_main(L, g, st, D, kmax, skip, variant);
+    return rc ? rc : launch_flush_tail(L, g, st, D, kmax);
+}
+
+int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant) {
     kmax = flush_kmax_supported(kmax);
     if (!kmax) return -1;
     if (variant < 0 || variant >= kNumFlushCfgs) variant = kmax == 64 ? kDefaultFlushCfg64 : kDefaultFlushCfg;
@@ -2478,11 +2495,7 @@ int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, in
 #undef LPG_FL_S
 #undef LPG_FL
     }
-    hipLaunchKernelGGL(k_flush_pivot_rows, dim3((unsigned)ntiles_p, (unsigned)kmax), dim3(kBlock), 0, stream, g.T, g, st,
-                       D.Pbuf, D.Cbuf, D.cs, D.rq);
-    if (hipGetLastError() != hipSuccess) return -1;
-    // the pending block is applied: clear it and the dequeue head
-    return hipMemsetAsync(&st->npend, 0, sizeof(int64_t) + sizeof(unsigned long long), stream) == hipSuccess ? 0 : -1;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 }  // namespace lpg

@@ -390,15 +390,16 @@ int main(int argc, char **argv) {
     double *Pbuf, *Cbuf;
     int64_t *rq;
     const int64_t cs = (m + 63) / 64 * 64;
-    CHK(hipMalloc(&Pbuf, (size_t)64 * ld * 8));
-    CHK(hipMalloc(&Cbuf, (size_t)64 * cs * 8));
-    CHK(hipMalloc(&rq, 64 * 8));
-    CHK(hipMemset(rq, 0xff, 64 * 8));                 // -1: no pivot row of the block is local
+    const int SL = 128;                                  // slots (blocks up to 128 pivots)
+    CHK(hipMalloc(&Pbuf, (size_t)SL * ld * 8));
+    CHK(hipMalloc(&Cbuf, (size_t)SL * cs * 8));
+    CHK(hipMalloc(&rq, SL * 8));
+    CHK(hipMemset(rq, 0xff, SL * 8));                 // -1: no pivot row of the block is local
     hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, L.T0, L.n, 1ull);
-    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, Pbuf, (int64_t)64 * ld, 2ull);
-    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, Cbuf, (int64_t)64 * cs, 3ull);
+    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, Pbuf, (int64_t)SL * ld, 2ull);
+    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, Cbuf, (int64_t)SL * cs, 3ull);
     const int64_t every = getenv("LAB_SCATTER") ? atoll(getenv("LAB_SCATTER")) : 0;
-    hipLaunchKernelGGL(k_zero_cols, dim3(1024), dim3(256), 0, 0, Pbuf, ld, nstruct + 1, ncols, 64, every);
+    hipLaunchKernelGGL(k_zero_cols, dim3(1024), dim3(256), 0, 0, Pbuf, ld, nstruct + 1, ncols, SL, every);
     CHK(hipDeviceSynchronize());
     L.g.T = L.T;
     L.g.ld = ld;
@@ -416,15 +417,22 @@ int main(int argc, char **argv) {
     CHK(hipEventCreate(&L.e1));
     printf("flush lab: %lld rows x %lld cols (ld %lld), K=%d, P zero for columns > %lld except every %lld-th\n",
            (long long)m, (long long)ncols, (long long)ld, L.K, (long long)nstruct, (long long)every);
+    const int reps = 5;
+    const char *only = getenv("LAB_ONLY");
+    auto want = [&](const char *nm) { return !only || strstr(nm, only); };
+    if (L.K > 64) {   // beyond the engine's blocks: timing only (no reference flush to compare with)
+#define WB(KM, R, NB, LB, PC)                                                                      \
+        if (L.K <= KM && want("w<" #KM "," #R "," #NB "," #LB "," #PC ">"))                        \
+            run(L, fn_w<KM, R, NB, LB, PC>, "w<" #KM "," #R "," #NB "," #LB "," #PC ">", false, reps);
+        WB(96, 512, 2, 2, 2) WB(96, 512, 2, 1, 1) WB(128, 512, 2, 1, 1) WB(128, 512, 2, 2, 2) WB(128, 1024, 2, 1, 1)
+        return 0;
+    }
     // reference result: the engine's default flush
     CHK(hipMemcpy(L.T, L.T0, L.n * 8, hipMemcpyDeviceToDevice));
     L.reset_state();
     fn_engine(L);
     CHK(hipDeviceSynchronize());
     CHK(hipMemcpy(L.Tref, L.T, L.n * 8, hipMemcpyDeviceToDevice));
-    const int reps = 5;
-    const char *only = getenv("LAB_ONLY");
-    auto want = [&](const char *nm) { return !only || strstr(nm, only); };
     for (int v : {8, 19, 20, 14, 16}) {
         g_variant = v;
         char nm[64];
