@@ -467,16 +467,14 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
             c->enq++;
             continue;
         }
-        if (D.on && c->fast_pivot) {            // deferred, with a communicator: prefetching prep, exchange, generic select
-            // (k_select_d under a communicator diverged from the oracle after a few pivots in the 2-rank
-            // test; the generic k_select is bitwise right there and is used instead)
+        if (D.on && c->fast_pivot) {            // deferred, with a communicator: the pair around the exchange
             if (launch_prep_dm(L, g, rule, c->st, s, c->cand, ncand_d, P, c->C[s], c->npp_d, D))
                 return fail(c, LPG_ERR_DEVICE, "prep launch failed");
             if ((rc = comm_allreduce_sum(c, P, (size_t)c->ld))) return rc;
             if (launch_price(L, g, rule, 1, c->st, s, P, c->C[s], c->pp, c->pc, c->npp, true))
                 return fail(c, LPG_ERR_DEVICE, "price launch failed");
-            if (launch_select(L, g, rule, false, c->st, s, s1, P, c->C[s], c->C[s1], c->pp, c->npp, c->basis, c->part,
-                              c->nsel_d, 0, -1, c->pc, c->skip, D))
+            if (launch_select_dm(L, g, rule, c->st, s, s1, c->C[s], c->C[s1], c->pp, c->npp, c->basis, c->part,
+                                 c->nsel_d, D))
                 return fail(c, LPG_ERR_DEVICE, "select launch failed");
             if ((rc = exchange_candidates(c))) return rc;
             if (++c->pend == c->defer_k && !c->capture_block)

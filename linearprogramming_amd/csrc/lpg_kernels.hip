@@ -442,6 +442,12 @@ __global__ __launch_bounds__(kBlock) void k_price(double *__restrict__ T, Geo g,
     }
     if (MODE == 1) count_live(pc, live);
     best = block_reduce_pp<RULE>(best);
+    // pad (the physical column) == j in caller order. Set it here: hipcc
+    // (ROCm 7.2) miscompiled the pad field of the inlined price_one's
+    // "if (better) best = c" in this kernel (pad kept the previous best's
+    // value while v, j, cls took the new one), which sent k_select_d to the
+    // neighbouring column under a communicator.
+    best.pad = (int32_t)best.j;
     if (threadIdx.x == 0) pp[blockIdx.x] = best;
 }
 
@@ -572,6 +578,7 @@ __global__ __launch_bounds__(kBlock) void k_prep(double *__restrict__ T, Geo g, 
     if (FUSE) {
         count_live(pc, live);
         pbest = block_reduce_pp<RULE>(pbest);
+        pbest.pad = (int32_t)pbest.j;    // caller order (see k_price)
         if (threadIdx.x == 0) pp[blockIdx.x] = pbest;
     }
 }
@@ -951,6 +958,9 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
         if (g.nobj == 2) *(d2 *)(T + rM * g.ld + 2 * j2) = dM;
         price_one<RULE>(pbest, dM.x, dR.x, lj.x, g, 2 * j2);
         price_one<RULE>(pbest, dM.y, dR.y, lj.y, g, 2 * j2 + 1);
+        // the physical column of this thread's winner, from its logical index
+        // (not through the struct select, see k_price)
+        pbest.pad = (int32_t)(pbest.j == lj.y ? 2 * j2 + 1 : 2 * j2);
     }
     LPG_PH(0, 4);
     pbest = block_argmin_pp<RULE, NT / 64>(pbest);
