@@ -186,3 +186,20 @@ def test_generic_and_prefetching_pivot_kernels_agree(lpg, monkeypatch, k, m, n, 
     assert res.pivots == fres.pivots == ores.pivots
     _assert_same(e, o, m)
     _assert_same(f, o, m)
+
+
+@pytest.mark.parametrize("nt", ["128", "256"])
+@pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1), (600, 1100, 3, 0, 0)])
+def test_pivot_block_sizes(lpg, monkeypatch, nt, m, n, seed, kind, rule):
+    """The deferred pair in 128- and 256-thread blocks (LPG_PIVOT_NT): the entering
+    column's physical index travels in PricePart.pad through every reduction, and
+    the whole solve must stay bitwise the oracle's."""
+    monkeypatch.setenv("LPG_PIVOT_NT", nt)
+    e = _engine(lpg, monkeypatch, 32, m, n + m + 1)
+    o = Oracle(m, n + m + 1)
+    e.generate(n, seed, kind)
+    o.generate(n, seed, kind)
+    res = e.solve(200_000, rule)
+    ores = o.solve(200_000, rule)
+    assert res.status == ores.status == 1 and res.pivots == ores.pivots
+    _assert_same(e, o, m)
