@@ -59,7 +59,7 @@ struct lpg_ctx {
     DevState *st = nullptr;
     int npp = 0, nsel = 0;
     int npp_d = 0, nsel_d = 0;    // the same partial counts for the single-rank deferred pair (k_prep_d / k_select_d)
-    int pivot_nt = kPivotThreads; // threads per block of that pair (LPG_PIVOT_NT)
+    int pivot_nt = kPivotThreads; // threads per block of that pair
     hipStream_t stream = nullptr;
     bool own_stream = false;
     // pivot-loop host state
@@ -239,6 +239,7 @@ static Defer defer_of(const lpg_ctx *c, int q) {
     d.kq = c->kq;
     d.lv = c->lv;
     d.colmap = c->colmap;
+    d.inv = c->inv;
     d.q = q;
     d.on = c->defer_k > 0 ? 1 : 0;
     return d;
@@ -639,8 +640,6 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->npp = price_blocks(g);
     const int64_t maxloc = (m + world - 1) / world + c->nobj;   // identical on every rank
     c->nsel = (int)std::min<int64_t>((maxloc + kBlock - 1) / kBlock, kMaxSelBlocks);
-    const char *pn = getenv("LPG_PIVOT_NT");
-    if (pn && world == 1) c->pivot_nt = atoi(pn) == 128 ? 128 : 256;
     c->npp_d = pivot_d_blocks(g, 0, c->pivot_nt);
     // k_select_d: one row per thread; with world > 1 the count must be the
     // same on every rank (the candidates are allgathered)

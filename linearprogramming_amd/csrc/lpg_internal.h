@@ -63,6 +63,7 @@ struct Defer {
     const double *zrow;       // ld zeros (the padding slots of the prefetching pivot kernels)
     int64_t *kq, *lv;         // K: entering / leaving variable of pending pivot q (logical; k_swap_plan)
     const int32_t *colmap;    // ld: logical column held by physical column p (k_prep_d's pricing keys)
+    const int32_t *inv;       // ld: physical column of logical column j (k_select_d when npp > its block)
     int      q;               // pending index of this pivot
     int      on;
 };
@@ -119,8 +120,8 @@ int launch_select(const Launch &L, const Geo &g, int rule, bool first, DevState 
 // One deferred-mode pivot without a communicator: k_prep_d + k_select_d
 // (prefetching forms of prep + select; candidates in and out through part).
 // Their grids: pivot_d_blocks(g, 0, nt) prep blocks (= pricing partials),
-// pivot_d_blocks(g, 1, nt) select blocks (= ratio candidates) of nt threads
-// (256 or 128; LPG_PIVOT_NT).
+// pivot_d_blocks(g, 1, nt) select blocks (= ratio candidates) of nt = 256
+// threads.
 constexpr int kPivotThreads = 256;
 int pivot_d_blocks(const Geo &g, int which, int nt);
 int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, Cand *part, int nsel,

@@ -1026,7 +1026,10 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
         }
         return;
     }
-    const int64_t kn = pb.j, kp = pb.pad;   // logical (log, basis, slot) and physical (loads) column
+    // logical (log, basis, slot) and physical (loads) column; with more partials
+    // than threads the round-1 loop selects structs again, and the physical
+    // column is then read through inv rather than trusted to that select (k_price)
+    const int64_t kn = pb.j, kp = npp > NT ? (int64_t)D.inv[kn] : (int64_t)pb.pad;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         dst->status = RUNNING;
         dst->k = kn;
@@ -1131,10 +1134,11 @@ int pivot_d_blocks(const Geo &g, int which, int nt) {
 int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, Cand *part, int nsel,
                    double *P, const double *Cs, double *Cs1, PricePart *pp, int npp, const int64_t *basis,
                    const Defer &D, int nt) {
-    // nt = 128 spreads the prefetch of the pending rows over twice the CUs
-    // (measured: no gain at config 3, 20.2 vs 20.4 us per pivot). One-wave
-    // blocks (nt = 64) gave wrong pivot rows at m >= 8192 and are not offered.
-    if ((nt != 128 && nt != 256) || npp != pivot_d_blocks(g, 0, nt) || nsel != pivot_d_blocks(g, 1, nt)) return -1;
+    // 256-thread blocks only: 64- and 128-thread forms were no faster at
+    // config 3 (17.8k / 18.9k vs 19.4k pivots/s) and diverged from the
+    // oracle at m = 16384 (first pivots identical, later ones not), so they
+    // are not offered.
+    if (nt != 256 || npp != pivot_d_blocks(g, 0, nt) || nsel != pivot_d_blocks(g, 1, nt)) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
 #define LPG_PD(R, PF, NT)                                                                                             \
     do {                                                                                                              \
@@ -1145,8 +1149,7 @@ int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s,
     } while (0)
 #define LPG_PD_NT(R, PF)                   \
     do {                                   \
-        if (nt == 128) LPG_PD(R, PF, 128); \
-        else LPG_PD(R, PF, 256);           \
+        LPG_PD(R, PF, 256);                \
     } while (0)
     const bool wide = D.q >= 32;            // pending chain longer than 32: the 64-slot prefetch forms
     if (rule == RULE_BLAND) {

@@ -188,18 +188,39 @@ def test_generic_and_prefetching_pivot_kernels_agree(lpg, monkeypatch, k, m, n, 
     _assert_same(f, o, m)
 
 
-@pytest.mark.parametrize("nt", ["128", "256"])
+@pytest.mark.parametrize("k", [32, 64])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1), (600, 1100, 3, 0, 0)])
-def test_pivot_block_sizes(lpg, monkeypatch, nt, m, n, seed, kind, rule):
-    """The deferred pair in 128- and 256-thread blocks (LPG_PIVOT_NT): the entering
-    column's physical index travels in PricePart.pad through every reduction, and
-    the whole solve must stay bitwise the oracle's."""
-    monkeypatch.setenv("LPG_PIVOT_NT", nt)
-    e = _engine(lpg, monkeypatch, 32, m, n + m + 1)
+def test_reordered_columns_to_optimality(lpg, monkeypatch, k, m, n, seed, kind, rule):
+    """Whole solves over many blocks: after every block the columns are reordered
+    (DESIGN.md §3.3), the entering column's physical index travels in
+    PricePart.pad through every reduction, and everything must stay bitwise the
+    oracle's."""
+    e = _engine(lpg, monkeypatch, k, m, n + m + 1)
     o = Oracle(m, n + m + 1)
     e.generate(n, seed, kind)
     o.generate(n, seed, kind)
     res = e.solve(200_000, rule)
     ores = o.solve(200_000, rule)
     assert res.status == ores.status == 1 and res.pivots == ores.pivots
+    _assert_same(e, o, m)
+
+
+@pytest.mark.parametrize("k", [32, 64])
+@pytest.mark.parametrize("rule,cap", [(0, 200_000), (1, 3000)])
+def test_wide_tableau_more_partials_than_threads(lpg, monkeypatch, k, rule, cap):
+    """ncols > 131072: k_prep_d leaves more pricing partials (two columns per
+    thread, 256 threads per block) than k_select_d has threads, so select
+    reduces them in a loop and reads the entering column's physical index
+    through inv (config 4's shape). Bland's rule needs ~41k
+    pivots here, so it stops at an iteration limit."""
+    m, n = 96, 140_000
+    e = _engine(lpg, monkeypatch, k, m, n + m + 1)
+    o = Oracle(m, n + m + 1, nthreads=8)
+    e.generate(n, 7, 0)
+    o.generate(n, 7, 0)
+    res = e.solve(cap, rule)
+    ores = o.solve(cap, rule)
+    assert res.status == ores.status and res.pivots == ores.pivots > k
+    assert res.status == (1 if rule == 0 else 4)
+    assert res.objective == ores.objective
     _assert_same(e, o, m)

@@ -14,7 +14,7 @@ o.generate(n, 20220518, 0)
 o.solve(K, 0)
 ok, orr = o.get_log()
 print("oracle", list(zip(ok.tolist(), orr.tolist())), flush=True)
-for defer, slow, nt in [("64", "0", "64"), ("64", "0", "256"), ("32", "0", "256"), ("64", "1", "64")]:
+for defer, slow, nt in [("64", "0", os.environ.get("LPG_PIVOT_NT", "256"))]:
         os.environ["LPG_DEFER"] = defer
         os.environ["LPG_SLOW_PIVOT"] = slow
         os.environ["LPG_PIVOT_NT"] = nt
