@@ -256,7 +256,8 @@ static bool reorders(const lpg_ctx *c) { return c->defer_k > 0 && c->fast_pivot 
 static int flush_launch(lpg_ctx *c) {
     int rc;
     const bool re = reorders(c);
-    if (re && launch_swap_plan(lau(c), c->st, c->kq, c->lv, c->colmap, c->inv, c->pairs))
+    if (re && (launch_swap_plan(lau(c), c->st, defer_of(c, 0), c->colmap, c->inv, c->pairs) ||
+               launch_move_cols(lau(c), geo(c), c->st, defer_of(c, 0), c->pairs)))
         return fail(c, LPG_ERR_DEVICE, "swap plan launch failed");
     if (c->timing && ((rc = timing_mark(c, 0)) || (rc = timing_mark(c, 1)))) return rc;
     if (launch_flush_main(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, c->skip, c->flush_variant))
@@ -265,7 +266,7 @@ static int flush_launch(lpg_ctx *c) {
     if (launch_flush_tail(lau(c), geo(c), c->st, defer_of(c, 0), c->pend))
         return fail(c, LPG_ERR_DEVICE, "flush launch failed");
     if (re) {
-        if (launch_swap_cols(lau(c), geo(c), c->pairs)) return fail(c, LPG_ERR_DEVICE, "swap launch failed");
+        if (launch_fill_cols(lau(c), geo(c), c->pairs)) return fail(c, LPG_ERR_DEVICE, "fill launch failed");
         c->permuted = true;
     }
     c->pend = 0;
@@ -680,7 +681,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         ALLOC(c->lv, (size_t)slots * sizeof(int64_t));
         ALLOC(c->colmap, (size_t)c->ld * sizeof(int32_t));
         ALLOC(c->inv, (size_t)c->ld * sizeof(int32_t));
-        ALLOC(c->pairs, (size_t)(1 + 2 * 64) * sizeof(int32_t));
+        ALLOC(c->pairs, (size_t)(1 + 3 * 64) * sizeof(int32_t));
     }
 #undef ALLOC
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);

@@ -147,10 +147,14 @@ int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0:
 // the physical positions the nonbasic columns had at the start of the solve
 // (for the synthetic LPs: one contiguous block) and a flush never meets
 // scattered live columns. launch_swap_plan (before the flush: reads npend)
-// pairs them and updates colmap / inv; launch_swap_cols (after) moves the data.
-int launch_swap_plan(const Launch &L, const DevState *st, const int64_t *kq, const int64_t *lv, int32_t *colmap,
-                     int32_t *inv, int32_t *pairs);
-int launch_swap_cols(const Launch &L, const Geo &g, const int32_t *pairs);
+// pairs them and updates colmap / inv; launch_move_cols (before the block
+// pass) moves the leaving columns' data and P entries into place;
+// launch_fill_cols (after the pivot-row rewrite) writes the entering
+// columns' unit vectors (lpg_kernels.hip, above k_swap_plan).
+int launch_swap_plan(const Launch &L, const DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
+                     int32_t *pairs);
+int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs);
+int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs);
 // Canonical order again: rows [i0, i0 + nr) gathered through inv into tmp
 // (nr x ld), then copied back; launch_iota resets colmap / inv.
 int launch_gather_rows(const Launch &L, const Geo &g, const int32_t *inv, double *tmp, int64_t i0, int64_t nr);

@@ -2185,15 +2185,33 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
 // are both "enter" went nonbasic -> basic (set E), both "leave": basic ->
 // nonbasic (set L); |E| == |L|. The i-th of E (in event order) trades
 // physical positions with the i-th of L. One wave; pairs[0] = count, then
-// (a, b) physical pairs.
+// triples (a, b, r): a = E's physical column, b = L's, r = the row E entered
+// on (its last event).
+//
+// The trade happens around the block pass, not after it, so the pass never
+// meets L's columns scattered over the basic region:
+//   k_move_cols (before): constraint rows take L's base column at a, the
+//     pending P rows take L's entries at a and +0 at b (b is then skipped by
+//     the pass); the objective rows, which are current, swap a and b.
+//   k_fill_cols (after the pass and the pivot-row rewrite): column b = E's
+//     final column, the unit vector e_r. Exactly: when E enters at pivot q,
+//     P_q[E] = piv / piv = 1 and every other row becomes fma(-x, 1, x) = +0;
+//     a later pivot u has P_u[E] = +0 / piv_u = +0 when piv_u > 0, so every
+//     row stays +0 (+0 + +-0 == +0) and row r stays 1. The plan therefore
+//     pairs nothing in a block holding a pivot element that is not positive
+//     (the forced pivots of lpg_pivot may be negative).
 // ------------------------------------------------------------------------
 
 __global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ st, const int64_t *__restrict__ kq,
-                                                  const int64_t *__restrict__ lv, int32_t *__restrict__ colmap,
-                                                  int32_t *__restrict__ inv, int32_t *__restrict__ pairs) {
+                                                  const int64_t *__restrict__ lv, const int64_t *__restrict__ rq,
+                                                  const double *__restrict__ Cbuf, int64_t cs,
+                                                  int32_t *__restrict__ colmap, int32_t *__restrict__ inv,
+                                                  int32_t *__restrict__ pairs) {
     const int np = (int)st->npend;
     const int q = threadIdx.x;
-    const int64_t x = q < np ? kq[q] : -1, y = q < np ? lv[q] : -1;
+    const int64_t x = q < np ? kq[q] : -1, y = q < np ? lv[q] : -1, rx = q < np ? rq[q] : -1;
+    // pivot element of pivot q: C_q[r_q]
+    const bool pos = q >= np || (rx >= 0 && Cbuf[(int64_t)q * cs + rx] > 0.0);
     __shared__ int64_t sk[64], sl[64];
     sk[q] = x;
     sl[q] = y;
@@ -2214,21 +2232,26 @@ __global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ s
             if (b == y && u < fy) { fy = u; fye = false; }
         }
     }
-    inE = inE && fxe;
-    inL = inL && !fye;
+    const bool allpos = __ballot(!pos) == 0ull;
+    inE = inE && fxe && allpos;
+    inL = inL && !fye && allpos;
     const unsigned long long me = __ballot(inE), ml = __ballot(inL);
     const unsigned long long below = (q == 0) ? 0ull : (~0ull >> (64 - q));
     const int ie = __popcll(me & below), il = __popcll(ml & below);
-    __shared__ int64_t eE[64], eL[64];
-    if (inE) eE[ie] = x;
+    __shared__ int64_t eE[64], eL[64], eR[64];
+    if (inE) {
+        eE[ie] = x;
+        eR[ie] = rx;
+    }
     if (inL) eL[il] = y;
     __syncthreads();
     const int n = __popcll(me);   // == __popcll(ml)
     if (q < n) {
         const int64_t ce = eE[q], cl = eL[q];
         const int32_t a = inv[ce], b = inv[cl];
-        pairs[1 + 2 * q] = a;
-        pairs[2 + 2 * q] = b;
+        pairs[1 + 3 * q] = a;
+        pairs[2 + 3 * q] = b;
+        pairs[3 + 3 * q] = (int32_t)eR[q];
         colmap[a] = (int32_t)cl;
         colmap[b] = (int32_t)ce;
         inv[cl] = a;
@@ -2237,44 +2260,77 @@ __global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ s
     if (q == 0) pairs[0] = n;
 }
 
-// one thread per row (constraint and objective rows) and group of 16 pairs
-// (blockIdx.y): swap the planned pairs
-__global__ __launch_bounds__(kBlock) void k_swap_cols(double *__restrict__ T, Geo g, const int32_t *__restrict__ pairs) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+// grid: (row blocks + 1, 4). One thread per row (constraint and objective
+// rows) and group of 16 pairs (blockIdx.y); the last x-block moves the
+// pending P entries.
+__global__ __launch_bounds__(kBlock) void k_move_cols(double *__restrict__ T, Geo g, const DevState *__restrict__ st,
+                                                      double *__restrict__ Pbuf, const int32_t *__restrict__ pairs) {
     const int n = pairs[0];
-    if (i >= g.nloc + g.nobj || n == 0) return;
+    if (n == 0) return;
+    if (blockIdx.x == gridDim.x - 1) {
+        if (blockIdx.y) return;
+        const int np = (int)st->npend;
+        for (int e = threadIdx.x; e < np * n; e += kBlock) {
+            const int q = e / n, p = e - q * n;
+            double *Pq = Pbuf + (int64_t)q * g.ld;
+            const int32_t a = pairs[1 + 3 * p], b = pairs[2 + 3 * p];
+            Pq[a] = Pq[b];
+            Pq[b] = 0.0;
+        }
+        return;
+    }
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= g.nloc + g.nobj) return;
+    const bool obj = i >= g.nloc;
     double *row = T + i * g.ld;
     for (int p0 = 16 * blockIdx.y; p0 < n; p0 += 16 * gridDim.y) {      // 16 pairs' loads in flight at once
         double va[16], vb[16];
         int ia[16], ib[16];
 #pragma unroll
         for (int u = 0; u < 16; u++) {
-            ia[u] = p0 + u < n ? pairs[1 + 2 * (p0 + u)] : 0;
-            ib[u] = p0 + u < n ? pairs[2 + 2 * (p0 + u)] : 0;
+            ia[u] = p0 + u < n ? pairs[1 + 3 * (p0 + u)] : 0;
+            ib[u] = p0 + u < n ? pairs[2 + 3 * (p0 + u)] : 0;
         }
 #pragma unroll
         for (int u = 0; u < 16; u++) {
-            va[u] = row[ia[u]];
             vb[u] = row[ib[u]];
+            va[u] = obj ? row[ia[u]] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 16; u++)
             if (p0 + u < n) {
                 row[ia[u]] = vb[u];
-                row[ib[u]] = va[u];
+                if (obj) row[ib[u]] = va[u];
             }
     }
 }
 
-int launch_swap_plan(const Launch &L, const DevState *st, const int64_t *kq, const int64_t *lv, int32_t *colmap,
-                     int32_t *inv, int32_t *pairs) {
-    hipLaunchKernelGGL(k_swap_plan, dim3(1), dim3(64), 0, (hipStream_t)L.stream, st, kq, lv, colmap, inv, pairs);
+// grid: (row blocks, 4): constraint row i, pairs p = blockIdx.y (mod 4)
+__global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Geo g, const int32_t *__restrict__ pairs) {
+    const int n = pairs[0];
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= g.nloc || n == 0) return;
+    double *row = T + i * g.ld;
+    for (int p = blockIdx.y; p < n; p += gridDim.y)
+        row[pairs[2 + 3 * p]] = (i == (int64_t)pairs[3 + 3 * p]) ? 1.0 : 0.0;
+}
+
+int launch_swap_plan(const Launch &L, const DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
+                     int32_t *pairs) {
+    hipLaunchKernelGGL(k_swap_plan, dim3(1), dim3(64), 0, (hipStream_t)L.stream, st, D.kq, D.lv, D.rq, D.Cbuf, D.cs,
+                       colmap, inv, pairs);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_swap_cols(const Launch &L, const Geo &g, const int32_t *pairs) {
+int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs) {
     const int64_t rows = g.nloc + g.nobj;
-    hipLaunchKernelGGL(k_swap_cols, dim3((unsigned)((rows + kBlock - 1) / kBlock), 4), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_move_cols, dim3((unsigned)((rows + kBlock - 1) / kBlock + 1), 4), dim3(kBlock), 0,
+                       (hipStream_t)L.stream, g.T, g, st, D.Pbuf, pairs);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs) {
+    hipLaunchKernelGGL(k_fill_cols, dim3((unsigned)((g.nloc + kBlock - 1) / kBlock), 4), dim3(kBlock), 0,
                        (hipStream_t)L.stream, g.T, g, pairs);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

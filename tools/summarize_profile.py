@@ -32,7 +32,7 @@ def _one(pattern):
 
 
 def short(name: str) -> str:
-    for key in ("k_flush_pivot_rows", "k_swap_plan", "k_swap_cols", "k_flush", "k_update", "k_select", "k_prep", "k_price", "k_generate", "k_basis_slack", "k_objective"):
+    for key in ("k_flush_pivot_rows", "k_swap_plan", "k_move_cols", "k_fill_cols", "k_flush", "k_update", "k_select", "k_prep", "k_price", "k_generate", "k_basis_slack", "k_objective"):
         if key in name:
             return key
     return name[:60]
