@@ -79,6 +79,7 @@ struct lpg_ctx {
     // basis-partitioned column order (single-rank deferred path, lpg_internal.h)
     int64_t *kq = nullptr, *lv = nullptr;   // per pending pivot: entering / leaving variable
     int32_t *colmap = nullptr, *inv = nullptr, *pairs = nullptr;
+    double *mul = nullptr;        // pivot-row multipliers of a flush (LPG_DEFER_MAX^2)
     double *tmp = nullptr;        // row chunk for canonicalize()
     int64_t tmp_rows = 0;
     bool permuted = false;        // colmap may differ from the identity
@@ -240,6 +241,7 @@ static Defer defer_of(const lpg_ctx *c, int q) {
     d.lv = c->lv;
     d.colmap = c->colmap;
     d.inv = c->inv;
+    d.mul = c->mul;
     d.q = q;
     d.on = c->defer_k > 0 ? 1 : 0;
     return d;
@@ -256,8 +258,8 @@ static bool reorders(const lpg_ctx *c) { return c->defer_k > 0 && c->fast_pivot 
 static int flush_launch(lpg_ctx *c) {
     int rc;
     const bool re = reorders(c);
-    if (re && (launch_swap_plan(lau(c), c->st, defer_of(c, 0), c->colmap, c->inv, c->pairs) ||
-               launch_move_cols(lau(c), geo(c), c->st, defer_of(c, 0), c->pairs)))
+    if (launch_swap_plan(lau(c), c->st, defer_of(c, 0), c->colmap, c->inv, c->pairs, re ? 1 : 0) ||
+        (re && launch_move_cols(lau(c), geo(c), c->st, defer_of(c, 0), c->pairs)))
         return fail(c, LPG_ERR_DEVICE, "swap plan launch failed");
     if (c->timing && ((rc = timing_mark(c, 0)) || (rc = timing_mark(c, 1)))) return rc;
     if (launch_flush_main(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, c->skip, c->flush_variant))
@@ -682,6 +684,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         ALLOC(c->colmap, (size_t)c->ld * sizeof(int32_t));
         ALLOC(c->inv, (size_t)c->ld * sizeof(int32_t));
         ALLOC(c->pairs, (size_t)(1 + 3 * 64) * sizeof(int32_t));
+        ALLOC(c->mul, (size_t)LPG_DEFER_MAX * LPG_DEFER_MAX * sizeof(double));
     }
 #undef ALLOC
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -769,7 +772,7 @@ void lpg_destroy(lpg_ctx *c) {
     for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
-                    c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->tmp};
+                    c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->mul, c->tmp};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);

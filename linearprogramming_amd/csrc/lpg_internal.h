@@ -64,6 +64,7 @@ struct Defer {
     int64_t *kq, *lv;         // K: entering / leaving variable of pending pivot q (logical; k_swap_plan)
     const int32_t *colmap;    // ld: logical column held by physical column p (k_prep_d's pricing keys)
     const int32_t *inv;       // ld: physical column of logical column j (k_select_d when npp > its block)
+    double  *mul;             // K x K: -C_u[r_q] (k_flush_pivot_rows' multipliers, built by k_swap_plan)
     int      q;               // pending index of this pivot
     int      on;
 };
@@ -137,7 +138,8 @@ int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int 
 // Apply the pending pivots (st->npend <= kmax) to constraint rows 0..nloc-1.
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant);
 // ... in two parts: the block pass itself (k_flushw / k_flushm / k_flush), then
-// the pivot-row rewrite and the pending-counter reset
+// the pivot-row rewrite and the pending-counter reset (the rewrite's
+// multipliers come from launch_swap_plan, launched before either part)
 int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant);
 int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax);
 int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0: k too large)
@@ -147,12 +149,13 @@ int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0:
 // the physical positions the nonbasic columns had at the start of the solve
 // (for the synthetic LPs: one contiguous block) and a flush never meets
 // scattered live columns. launch_swap_plan (before the flush: reads npend)
-// pairs them and updates colmap / inv; launch_move_cols (before the block
+// pairs them and updates colmap / inv when plan != 0, and always builds the
+// pivot-row multipliers D.mul; launch_move_cols (before the block
 // pass) moves the leaving columns' data and P entries into place;
 // launch_fill_cols (after the pivot-row rewrite) writes the entering
 // columns' unit vectors (lpg_kernels.hip, above k_swap_plan).
 int launch_swap_plan(const Launch &L, const DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
-                     int32_t *pairs);
+                     int32_t *pairs, int plan);
 int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs);
 int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs);
 // Canonical order again: rows [i0, i0 + nr) gathered through inv into tmp

@@ -2145,38 +2145,58 @@ __global__ __launch_bounds__(kBlock, LB) void k_flushw(double *__restrict__ T, G
     if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
 }
 
-// The pivot rows of the block, after k_flush: row r_q (last occurrence q in
-// the block) = P_q, continued by the chain of the later pivots. These values
-// do not depend on T_base, so the rows k_flush wrote without the replacement
-// are simply overwritten. grid: (column tiles of 256, KMAX slots).
+// The pivot rows of the block, after the block pass: row r_q (q its last
+// pivot in the block) = P_q continued by the chain of the later pivots,
+// x = fma(mul[q][u], P_u[j], x) for u = q+1 .. np-1 (mul[q][u] = -C_u[r_q],
+// built by k_swap_plan). These values do not depend on T_base, so the rows
+// the pass wrote without the replacement are simply overwritten. A block
+// takes 64 columns and every pivot row: the block's P entries and the
+// multipliers are staged in LDS once, so each P entry leaves HBM once (the
+// per-row form re-read P_u for every earlier pivot row: 98 us at config 3).
 __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict__ T, Geo g,
                                                              const DevState *__restrict__ st,
                                                              const double *__restrict__ Pbuf,
-                                                             const double *__restrict__ Cbuf, int64_t cs,
+                                                             const double *__restrict__ mul,
                                                              const int64_t *__restrict__ rq) {
+    constexpr int K = LPG_DEFER_MAX;
+    constexpr int PW = K / (kBlock / 64);               // P rows staged per wave
+    constexpr int MT = K * K / kBlock;                  // multipliers staged per thread
+    __shared__ double sP[K][64];
+    __shared__ double sM[K * K];
     const int np = (int)st->npend;
-    const int q = blockIdx.y;
-    if (q >= np) return;
-    const int64_t r = rq[q];
-    if (r < 0) return;                                  // pivot row on another rank
-    const int lane = threadIdx.x & 63;
-    // lane u holds r_u and the multiplier -C_u[r] of a later pivot u (-0 elsewhere)
-    const int64_t ru = lane < np ? rq[lane] : -1;
-    if (__ballot(lane > q && ru == r)) return;          // a later pivot replaces this row again
-    const double cl = (lane > q && lane < np) ? -Cbuf[(int64_t)lane * cs + r] : -0.0;
-    const uint64_t clb = (uint64_t)__double_as_longlong(cl);
-    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (np <= 0) return;
+    const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t j = (int64_t)blockIdx.x * 64 + c;
     const bool ok = j < g.ncols;
-    double x = ok ? Pbuf[(int64_t)q * g.ld + j] : 0.0;
-    for (int q0 = q + 1; q0 < np; q0 += 16) {          // 16 pivots' loads in flight at once
-        double v[16];
+    {
+        double v[PW], m[MT];
 #pragma unroll
-        for (int u = 0; u < 16; u++) v[u] = (ok && q0 + u < np) ? Pbuf[(int64_t)(q0 + u) * g.ld + j] : 0.0;
+        for (int k = 0; k < PW; k++) {
+            const int u = w + 4 * k;
+            v[k] = (ok && u < np) ? Pbuf[(int64_t)u * g.ld + j] : 0.0;
+        }
 #pragma unroll
-        for (int u = 0; u < 16; u++)
-            if (q0 + u < np) x = fma(__longlong_as_double((long long)rdl64(clb, q0 + u)), v[u], x);
+        for (int k = 0; k < MT; k++) {
+            const int e = threadIdx.x + kBlock * k;
+            m[k] = (e >> 6) < np ? mul[e] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < PW; k++) sP[w + 4 * k][c] = v[k];
+#pragma unroll
+        for (int k = 0; k < MT; k++) sM[threadIdx.x + kBlock * k] = m[k];
     }
-    if (ok) T[r * g.ld + j] = x;
+    const int64_t ru = c < np ? rq[c] : -1;             // lane u: r_u
+    __syncthreads();
+    for (int q = w; q < np; q += 4) {
+        const int64_t r = (int64_t)rdl64((uint64_t)ru, q);
+        if (r < 0) continue;                            // pivot row on another rank
+        if (__ballot(c > q && ru == r)) continue;       // a later pivot replaces this row again
+        double x = sP[q][c];
+        const double *mq = sM + q * K;
+#pragma unroll 4
+        for (int u = q + 1; u < np; u++) x = fma(mq[u], sP[u][c], x);
+        if (ok) T[r * g.ld + j] = x;
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -2202,12 +2222,35 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
 //     (the forced pivots of lpg_pivot may be negative).
 // ------------------------------------------------------------------------
 
+// grid: 1 + kMulBlocks blocks of one wave. Block 0: the column plan (when
+// plan != 0). Blocks 1..: the multipliers of k_flush_pivot_rows,
+// mul[q][u] = -C_u[r_q] for u > q (+0 elsewhere), rows of LPG_DEFER_MAX.
+constexpr int kMulBlocks = 8;
 __global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ st, const int64_t *__restrict__ kq,
                                                   const int64_t *__restrict__ lv, const int64_t *__restrict__ rq,
                                                   const double *__restrict__ Cbuf, int64_t cs,
                                                   int32_t *__restrict__ colmap, int32_t *__restrict__ inv,
-                                                  int32_t *__restrict__ pairs) {
+                                                  int32_t *__restrict__ pairs, double *__restrict__ mul, int plan) {
     const int np = (int)st->npend;
+    if (blockIdx.x > 0) {
+        constexpr int QB = LPG_DEFER_MAX / kMulBlocks;       // pivot rows per block
+        const int u = threadIdx.x;
+        const int q0 = (blockIdx.x - 1) * QB;
+        int64_t r[QB];
+        double v[QB];
+#pragma unroll
+        for (int k = 0; k < QB; k++) r[k] = q0 + k < np ? rq[q0 + k] : -1;
+#pragma unroll
+        for (int k = 0; k < QB; k++) {
+            const int q = q0 + k;
+            v[k] = (u > q && u < np && r[k] >= 0) ? -Cbuf[(int64_t)u * cs + r[k]] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < QB; k++)
+            if (q0 + k < np) mul[(q0 + k) * LPG_DEFER_MAX + u] = v[k];
+        return;
+    }
+    if (!plan) return;
     const int q = threadIdx.x;
     const int64_t x = q < np ? kq[q] : -1, y = q < np ? lv[q] : -1, rx = q < np ? rq[q] : -1;
     // pivot element of pivot q: C_q[r_q]
@@ -2316,9 +2359,9 @@ __global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Ge
 }
 
 int launch_swap_plan(const Launch &L, const DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
-                     int32_t *pairs) {
-    hipLaunchKernelGGL(k_swap_plan, dim3(1), dim3(64), 0, (hipStream_t)L.stream, st, D.kq, D.lv, D.rq, D.Cbuf, D.cs,
-                       colmap, inv, pairs);
+                     int32_t *pairs, int plan) {
+    hipLaunchKernelGGL(k_swap_plan, dim3(1 + kMulBlocks), dim3(64), 0, (hipStream_t)L.stream, st, D.kq, D.lv, D.rq,
+                       D.Cbuf, D.cs, colmap, inv, pairs, D.mul, plan);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2419,16 +2462,17 @@ int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &
     kmax = flush_kmax_supported(kmax);
     if (!kmax) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
-    const int64_t ntiles_p = (g.ncols + kBlock - 1) / kBlock;   // k_flush_pivot_rows column tiles
-    hipLaunchKernelGGL(k_flush_pivot_rows, dim3((unsigned)ntiles_p, (unsigned)kmax), dim3(kBlock), 0, stream, g.T, g, st,
-                       D.Pbuf, D.Cbuf, D.cs, D.rq);
+    const int64_t ntiles_p = (g.ncols + 63) / 64;   // k_flush_pivot_rows column tiles
+    hipLaunchKernelGGL(k_flush_pivot_rows, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st, D.Pbuf, D.mul,
+                       D.rq);
     if (hipGetLastError() != hipSuccess) return -1;
     // the pending block is applied: clear it and the dequeue head
     return hipMemsetAsync(&st->npend, 0, sizeof(int64_t) + sizeof(unsigned long long), stream) == hipSuccess ? 0 : -1;
 }
 
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant) {
-    int rc = launch_flush_main(L, g, st, D, kmax, skip, variant);
+    int rc = launch_swap_plan(L, st, D, nullptr, nullptr, nullptr, 0);   // the multipliers only
+    if (!rc) rc = launch_flush_main(L, g, st, D, kmax, skip, variant);
     return rc ? rc : launch_flush_tail(L, g, st, D, kmax);
 }
 

@@ -412,6 +412,7 @@ int main(int argc, char **argv) {
     L.D.Cbuf = Cbuf;
     L.D.cs = cs;
     L.D.rq = rq;
+    CHK(hipMalloc(&L.D.mul, (size_t)LPG_DEFER_MAX * LPG_DEFER_MAX * 8));
     L.D.on = 1;
     CHK(hipEventCreate(&L.e0));
     CHK(hipEventCreate(&L.e1));
