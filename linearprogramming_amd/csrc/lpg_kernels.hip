@@ -2147,12 +2147,16 @@ __global__ __launch_bounds__(kBlock, LB) void k_flushw(double *__restrict__ T, G
 
 // The pivot rows of the block, after the block pass: row r_q (q its last
 // pivot in the block) = P_q continued by the chain of the later pivots,
-// x = fma(mul[q][u], P_u[j], x) for u = q+1 .. np-1 (mul[q][u] = -C_u[r_q],
+// x = fma(mul[u][q], P_u[j], x) for u = q+1 .. np-1 (mul[u][q] = -C_u[r_q],
 // built by k_swap_plan). These values do not depend on T_base, so the rows
 // the pass wrote without the replacement are simply overwritten. A block
 // takes 64 columns and every pivot row: the block's P entries and the
 // multipliers are staged in LDS once, so each P entry leaves HBM once (the
 // per-row form re-read P_u for every earlier pivot row: 98 us at config 3).
+// Each wave runs groups of 4 consecutive rows, so one LDS read of P_u[j]
+// feeds 4 chains (groups {w, 7-w, 8+w, 15-w}: equal work per wave); the
+// first steps of a group, where only some of its rows have started, are
+// peeled so that every row sees exactly its own steps.
 __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict__ T, Geo g,
                                                              const DevState *__restrict__ st,
                                                              const double *__restrict__ Pbuf,
@@ -2162,7 +2166,7 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
     constexpr int PW = K / (kBlock / 64);               // P rows staged per wave
     constexpr int MT = K * K / kBlock;                  // multipliers staged per thread
     __shared__ double sP[K][64];
-    __shared__ double sM[K * K];
+    __shared__ __attribute__((aligned(32))) double sM[K * K];   // [u][q]
     const int np = (int)st->npend;
     if (np <= 0) return;
     const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -2187,15 +2191,51 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
     }
     const int64_t ru = c < np ? rq[c] : -1;             // lane u: r_u
     __syncthreads();
-    for (int q = w; q < np; q += 4) {
-        const int64_t r = (int64_t)rdl64((uint64_t)ru, q);
-        if (r < 0) continue;                            // pivot row on another rank
-        if (__ballot(c > q && ru == r)) continue;       // a later pivot replaces this row again
-        double x = sP[q][c];
-        const double *mq = sM + q * K;
-#pragma unroll 4
-        for (int u = q + 1; u < np; u++) x = fma(mq[u], sP[u][c], x);
-        if (ok) T[r * g.ld + j] = x;
+    static_assert(K == 64 && kBlock == 256, "4 waves x 4 groups of 4 rows");
+#pragma unroll 1
+    for (int k = 0; k < 4; k++) {
+        const int grp = (k & 1) ? 8 * (k >> 1) + 7 - w : 8 * (k >> 1) + w;
+        const int q0 = 4 * grp;
+        if (q0 >= np) continue;                         // uniform
+        double x0 = sP[q0][c], x1 = sP[q0 + 1][c], x2 = sP[q0 + 2][c], x3 = sP[q0 + 3][c];
+        auto m4 = [&](int u) { return *(const d4 *)(sM + u * K + q0); };   // mul[u][q0 .. q0 + 3]
+        if (q0 + 1 < np) {
+            const double p = sP[q0 + 1][c];
+            const d4 m = m4(q0 + 1);
+            x0 = fma(m[0], p, x0);
+        }
+        if (q0 + 2 < np) {
+            const double p = sP[q0 + 2][c];
+            const d4 m = m4(q0 + 2);
+            x0 = fma(m[0], p, x0);
+            x1 = fma(m[1], p, x1);
+        }
+        if (q0 + 3 < np) {
+            const double p = sP[q0 + 3][c];
+            const d4 m = m4(q0 + 3);
+            x0 = fma(m[0], p, x0);
+            x1 = fma(m[1], p, x1);
+            x2 = fma(m[2], p, x2);
+        }
+#pragma unroll 2
+        for (int u = q0 + 4; u < np; u++) {
+            const double p = sP[u][c];
+            const d4 m = m4(u);
+            x0 = fma(m[0], p, x0);
+            x1 = fma(m[1], p, x1);
+            x2 = fma(m[2], p, x2);
+            x3 = fma(m[3], p, x3);
+        }
+        const double xs[4] = {x0, x1, x2, x3};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int q = q0 + i;
+            if (q >= np) break;                         // uniform
+            const int64_t r = (int64_t)rdl64((uint64_t)ru, q);
+            if (r < 0) continue;                        // pivot row on another rank
+            if (__ballot(c > q && ru == r)) continue;   // a later pivot replaces this row again
+            if (ok) T[r * g.ld + j] = xs[i];
+        }
     }
 }
 
@@ -2224,7 +2264,7 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
 
 // grid: 1 + kMulBlocks blocks of one wave. Block 0: the column plan (when
 // plan != 0). Blocks 1..: the multipliers of k_flush_pivot_rows,
-// mul[q][u] = -C_u[r_q] for u > q (+0 elsewhere), rows of LPG_DEFER_MAX.
+// mul[u][q] = -C_u[r_q] for u > q (+0 elsewhere), rows of LPG_DEFER_MAX.
 constexpr int kMulBlocks = 8;
 __global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ st, const int64_t *__restrict__ kq,
                                                   const int64_t *__restrict__ lv, const int64_t *__restrict__ rq,
@@ -2232,22 +2272,20 @@ __global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ s
                                                   int32_t *__restrict__ colmap, int32_t *__restrict__ inv,
                                                   int32_t *__restrict__ pairs, double *__restrict__ mul, int plan) {
     const int np = (int)st->npend;
-    if (blockIdx.x > 0) {
-        constexpr int QB = LPG_DEFER_MAX / kMulBlocks;       // pivot rows per block
-        const int u = threadIdx.x;
-        const int q0 = (blockIdx.x - 1) * QB;
-        int64_t r[QB];
-        double v[QB];
+    if (blockIdx.x > 0) {                                   // mul[u][q], lane q
+        constexpr int UB = LPG_DEFER_MAX / kMulBlocks;       // pivots u per block
+        const int q = threadIdx.x;
+        const int u0 = (blockIdx.x - 1) * UB;
+        const int64_t r = q < np ? rq[q] : -1;
+        double v[UB];
 #pragma unroll
-        for (int k = 0; k < QB; k++) r[k] = q0 + k < np ? rq[q0 + k] : -1;
-#pragma unroll
-        for (int k = 0; k < QB; k++) {
-            const int q = q0 + k;
-            v[k] = (u > q && u < np && r[k] >= 0) ? -Cbuf[(int64_t)u * cs + r[k]] : 0.0;
+        for (int k = 0; k < UB; k++) {
+            const int u = u0 + k;
+            v[k] = (u > q && u < np && r >= 0) ? -Cbuf[(int64_t)u * cs + r] : 0.0;
         }
 #pragma unroll
-        for (int k = 0; k < QB; k++)
-            if (q0 + k < np) mul[(q0 + k) * LPG_DEFER_MAX + u] = v[k];
+        for (int k = 0; k < UB; k++)
+            if (u0 + k < np) mul[(u0 + k) * LPG_DEFER_MAX + q] = v[k];
         return;
     }
     if (!plan) return;
@@ -2255,16 +2293,13 @@ __global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ s
     const int64_t x = q < np ? kq[q] : -1, y = q < np ? lv[q] : -1, rx = q < np ? rq[q] : -1;
     // pivot element of pivot q: C_q[r_q]
     const bool pos = q >= np || (rx >= 0 && Cbuf[(int64_t)q * cs + rx] > 0.0);
-    __shared__ int64_t sk[64], sl[64];
-    sk[q] = x;
-    sl[q] = y;
-    __syncthreads();
     // x (entering at q) is in E iff no later event touches x and its first event is an entry
     bool inE = q < np, inL = q < np;
     int fx = q, fy = q;           // first event index of x / y, and its kind
     bool fxe = true, fye = false;
     for (int u = 0; u < np; u++) {
-        const int64_t a = sk[u], b = sl[u];
+        // event u from lane u (x, y computed with EXEC full)
+        const int64_t a = (int64_t)rdl64((uint64_t)x, u), b = (int64_t)rdl64((uint64_t)y, u);
         if (u > q) {
             if (a == x || b == x) inE = false;
             if (a == y || b == y) inL = false;
