@@ -2030,18 +2030,22 @@ __global__ __launch_bounds__(kBlock) void k_flushs(double *__restrict__ T, Geo g
 // for 64 slots) and restarts its pipeline per item: 2.36 ms vs 1.64 ms for
 // this kernel at config 3, K = 64 (tools/flush_lab.hip,
 // profiles/r01_flush_lab_k64.log). Same chain, same MFMA, bitwise identical.
-template <int KMAX, int NB, int LB>
-__global__ __launch_bounds__(kBlock, LB) void k_flushw(double *__restrict__ T, Geo g, DevState *__restrict__ st,
-                                                       const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
-                                                       int64_t cs, int64_t ntiles, int64_t nitems, int64_t rows,
-                                                       int skip) {
+// WPB waves per block: a tile is 32 * WPB columns wide, and every column
+// tile reads all of C once (WPB = 8 halves that on-chip traffic: C is
+// 8.4 MB at config 3, read by every tile from the Infinity Cache).
+template <int KMAX, int NB, int LB, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                         const double *__restrict__ Pbuf,
+                                                         const double *__restrict__ Cbuf, int64_t cs, int64_t ntiles,
+                                                         int64_t nitems, int64_t rows, int skip) {
+    constexpr int NTH = 64 * WPB;
     constexpr int G = KMAX / 4;
     constexpr int BAND = KMAX * 16;                 // doubles per band
-    constexpr int PER = BAND / 2 / kBlock;          // 16-byte multiplier pieces per thread per band
-    static_assert(PER >= 1 && BAND / 2 % kBlock == 0, "band staging");
+    constexpr int PER = BAND / 2 / NTH;             // 16-byte multiplier pieces per thread per band
+    static_assert(PER >= 1 && BAND / 2 % NTH == 0, "band staging");
     __shared__ __attribute__((aligned(16))) double sC[NB][BAND];
     __shared__ int64_t next_item;
-    __shared__ int wsum[kBlock / 64];
+    __shared__ int wsum[WPB];
     const int np = (int)st->npend;
     if (np <= 0) return;
     const int64_t ld = g.ld;
@@ -2057,8 +2061,8 @@ __global__ __launch_bounds__(kBlock, LB) void k_flushw(double *__restrict__ T, G
         const int64_t tile = item % ntiles, strip = item / ntiles;
         const int64_t i0 = strip * rows;
         const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
-        const int64_t cl = tile * 128 + wave * 32 + 2 * lc;   // this lane's column pair
-        const bool in = cl < g.ncols;                         // cl even, ld even: cl + 1 < ld
+        const int64_t cl = tile * (32 * WPB) + wave * 32 + 2 * lc;   // this lane's column pair
+        const bool in = cl < g.ncols;                                // cl even, ld even: cl + 1 < ld
         double be[G], bo[G];
         bool live = false;
 #pragma unroll
@@ -2080,15 +2084,19 @@ __global__ __launch_bounds__(kBlock, LB) void k_flushw(double *__restrict__ T, G
         const bool wlive = mine > 0;                                   // wave-uniform
         if (lane == 0) wsum[wave] = mine;
         if (__syncthreads_count(wlive && lane == 0) == 0) continue;    // the whole tile is skipped
-        if (threadIdx.x == 0)
-            touched += (unsigned long long)(wsum[0] + wsum[1] + wsum[2] + wsum[3]) * (unsigned long long)(i1 - i0);
+        if (threadIdx.x == 0) {
+            int sum = 0;
+#pragma unroll
+            for (int w = 0; w < WPB; w++) sum += wsum[w];
+            touched += (unsigned long long)sum * (unsigned long long)(i1 - i0);
+        }
         const int nb = (int)((i1 - i0 + 15) / 16);
         // multiplier piece e of band s: slot q = e / 8, band rows 2 (e % 8) .. +1
         // (zeros past np and past i1: A = -0 there, x + -0 == x)
         auto cload = [&](d2 (&cr)[PER], int s) {
 #pragma unroll
             for (int u = 0; u < PER; u++) {
-                const int e = threadIdx.x + u * kBlock;
+                const int e = threadIdx.x + u * NTH;
                 const int q = e >> 3, rr = 2 * (e & 7);
                 const int64_t row = i0 + 16 * s + rr;
                 d2 v = d2{0.0, 0.0};
@@ -2098,7 +2106,7 @@ __global__ __launch_bounds__(kBlock, LB) void k_flushw(double *__restrict__ T, G
         };
         auto cstore = [&](const d2 (&cr)[PER], int s) {
 #pragma unroll
-            for (int u = 0; u < PER; u++) *(d2 *)(&sC[s % NB][2 * (threadIdx.x + u * kBlock)]) = cr[u];
+            for (int u = 0; u < PER; u++) *(d2 *)(&sC[s % NB][2 * (threadIdx.x + u * NTH)]) = cr[u];
         };
         for (int s = 0; s < NB - 1; s++) {   // prologue: bands 0 .. NB-2 into the ring
             d2 cr[PER];
@@ -2477,6 +2485,10 @@ static const FlushCfg kFlushCfgs[] = {
     {3, 3, true, true, 512, 0},     // 22 same, 3-deep ring
     {3, 2, true, true, 256, 0},     // 23 256-row items
     {3, 2, true, true, 1024, 0},    // 24 1024-row items
+    {3, 2, true, true, 512, 8},     // 25 k_flushw, 8-wave blocks (256-column tiles; 4 waves below 64 slots)
+    {3, 2, true, true, 1024, 8},    // 26 same, 1024-row items
+    {3, 3, true, true, 512, 8},     // 27 same, 3-deep ring
+    {3, 2, true, true, 256, 8},     // 28 same, 256-row items
 };
 constexpr int kNumFlushCfgs = sizeof(kFlushCfgs) / sizeof(kFlushCfgs[0]);
 constexpr int kDefaultFlushCfg = 8;       // blocks of <= 32 pivots: k_flushm
@@ -2517,22 +2529,27 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
     if (variant < 0 || variant >= kNumFlushCfgs) variant = kmax == 64 ? kDefaultFlushCfg64 : kDefaultFlushCfg;
     FlushCfg cfg = kFlushCfgs[variant];
     hipStream_t stream = (hipStream_t)L.stream;
-    const int64_t ntiles_p = (g.ncols + kBlock - 1) / kBlock;   // k_flush_pivot_rows column tiles
-    if (cfg.mfma == 3) {                                     // k_flushw: ru = ring depth, strip = rows per item
-        const int64_t ntiles = (g.ncols + 127) / 128;
+    if (cfg.mfma == 3) {                                     // k_flushw: ru = ring depth, strip = rows per item,
+        const int wpb = (cfg.per_cu == 8 && kmax == 64) ? 8 : 4;   // per_cu = waves per block
+        const int64_t ntiles = (g.ncols + 32 * wpb - 1) / (32 * wpb);
         int64_t rows = cfg.strip;
-        while (rows > 64 && ntiles * ((g.nloc + rows - 1) / rows) < 2048) rows /= 2;   // small tableaus: fill the chip
+        while (rows > 64 && ntiles * ((g.nloc + rows - 1) / rows) < 2048 / (wpb / 4)) rows /= 2;   // small tableaus: fill the chip
         const int64_t nitems = ntiles * ((g.nloc + rows - 1) / rows);
-        const int lb = kmax == 64 ? 2 : 3;                   // VGPRs: 184 at 64 slots, <= 128 below (8-32: the 32 form)
+        // VGPRs: 184 at 64 slots, <= 128 below (8-32: the 32 form); 8-wave blocks: one per CU
+        const int lb = wpb == 8 ? 1 : kmax == 64 ? 2 : 3;
         const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * lb);
         if (nblocks < 1) return 0;
-#define LPG_FW(K, NB, LBV)                                                                                            \
-    hipLaunchKernelGGL((k_flushw<K, NB, LBV>), dim3((unsigned)nblocks), dim3(kBlock), 0, stream, g.T, g, st, D.Pbuf, \
-                       D.Cbuf, D.cs, ntiles, nitems, rows, skip)
+#define LPG_FW(K, NB, LBV, W)                                                                                     \
+    hipLaunchKernelGGL((k_flushw<K, NB, LBV, W>), dim3((unsigned)nblocks), dim3(64 * W), 0, stream, g.T, g, st, \
+                       D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip)
 #define LPG_FW_K(NB)                                  \
-    switch (kmax) {                                   \
-        case 64: LPG_FW(64, NB, 2); break;            \
-        default: LPG_FW(32, NB, 3); break;            \
+    if (wpb == 8) {                                   \
+        LPG_FW(64, NB, 1, 8);                         \
+    } else {                                          \
+        switch (kmax) {                               \
+            case 64: LPG_FW(64, NB, 2, 4); break;     \
+            default: LPG_FW(32, NB, 3, 4); break;     \
+        }                                             \
     }
         if (cfg.ru == 3) { LPG_FW_K(3) }
         else { LPG_FW_K(2) }
@@ -2606,7 +2623,7 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
 #undef LPG_FM_S
 #undef LPG_FM
     } else {
-        const int64_t ntiles = ntiles_p;
+        const int64_t ntiles = (g.ncols + kBlock - 1) / kBlock;   // columns of 256
         // small tableaus: 32-row strips so that the items fill the chip
         if (ntiles * ((g.nloc + cfg.strip - 1) / cfg.strip) < 4096) cfg.strip = 32;
         // the LDS tile is KMAX x strip doubles: keep it within 64 KB

@@ -105,7 +105,7 @@ def test_enqueue_past_optimal_partial_block(lpg, monkeypatch):
 
 
 @pytest.mark.parametrize("k", [32, 64])
-@pytest.mark.parametrize("variant", list(range(25)))
+@pytest.mark.parametrize("variant", list(range(29)))
 def test_flush_variants_identical(lpg, monkeypatch, variant, k):
     monkeypatch.setenv("LPG_FLUSH_VARIANT", str(variant))
     m, n = 300, 700
@@ -151,11 +151,11 @@ def test_bad_block_size(lpg, monkeypatch):
         lpg.Engine(8, 20)
 
 
-@pytest.mark.parametrize("variant", [7, 8, 9, 14, 15, 19, 21, 22, 23])
+@pytest.mark.parametrize("variant", [7, 8, 9, 14, 15, 19, 21, 22, 23, 25, 26])
 @pytest.mark.parametrize("k", [3, 8, 32, 64])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1)])
 def test_flush_kernels_block_sizes(lpg, monkeypatch, variant, k, m, n, seed, kind, rule):
-    """VALU (7), matrix-core (8, 9, 14, 15, 19) and tall-item banded (21-23)
+    """VALU (7), matrix-core (8, 9, 14, 15, 19) and tall-item banded (21-23; 25-26 8-wave blocks)
     flushes at every compiled block bound, to optimality, against the oracle
     (odd shapes: ragged column tiles, strips and bands)."""
     monkeypatch.setenv("LPG_FLUSH_VARIANT", str(variant))
