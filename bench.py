@@ -206,6 +206,7 @@ def main():
     eng.set_timing(live_events)
     if live_events:
         eng.get_timing()                               # reset sums
+    eng.prepare(lpg.RULE_DANTZIG)                      # the replayed graph is built here, not in the timed region
     if world > 1:
         dist.barrier()
     eng.device_sync()

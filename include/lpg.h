@@ -189,6 +189,13 @@ int  lpg_sync(lpg_ctx *ctx, lpg_result *out);
 /* Pre-size the device pivot log for npivots more pivots so that no
  * reallocation (and host synchronisation) happens inside a timed region. */
 int  lpg_reserve_log(lpg_ctx *ctx, int64_t npivots);
+/* Build, ahead of the pivot loop, the replayed HIP graph that lpg_enqueue /
+ * lpg_solve use for runs of at least two blocks under this rule (capture +
+ * instantiate, ~0.5 ms of host time), so that it does not land inside a timed
+ * region. No pivot runs; a pending deferred block is applied first. A no-op
+ * where the loop does not replay graphs (graphs disabled, eager timing, a
+ * host communicator). */
+int  lpg_prepare(lpg_ctx *ctx, int rule);
 
 /* Apply one caller-chosen pivot (entering column k, 1-based; leaving row r,
  * 0-based) with the same arithmetic as the loop; |T[r][k]| must exceed

@@ -79,6 +79,7 @@ PROTOTYPES = [
     ("lpg_enqueue", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]),
     ("lpg_sync", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Result)]),
     ("lpg_reserve_log", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    ("lpg_prepare", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("lpg_pivot", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]),
     ("lpg_solve_two_phase", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, c_double_p, ctypes.c_int64, ctypes.c_int,
                                            ctypes.POINTER(Result)]),

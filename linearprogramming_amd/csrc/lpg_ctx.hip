@@ -921,6 +921,26 @@ int lpg_reserve_log(lpg_ctx *c, int64_t npivots) {
     return ensure_log(c, c->enq + npivots);
 }
 
+int lpg_prepare(lpg_ctx *c, int rule) {
+    if (!c || (rule != LPG_RULE_DANTZIG && rule != LPG_RULE_BLAND)) return fail(c, LPG_ERR_ARG, "lpg_prepare: bad arguments");
+    int rc;
+    if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
+    if (!c->booted || c->boot_rule != rule)
+        if ((rc = bootstrap(c, rule))) return rc;
+    // the conditions under which enqueue replays graphs (enqueue, above)
+    const int G = graph_len(c);
+    const bool timed = c->timing && c->defer_k == 0;
+    const bool comm_ok = !has_comm(c) || (c->nccl && !c->have_hops && c->graph_comm);
+    if (!c->use_graphs || timed || !comm_ok || (G & 1)) return 0;
+    if (c->graph[c->par] && c->graph_rule[c->par] == rule) return 0;
+    if ((rc = graph_build(c, rule))) {
+        if (!has_comm(c)) return rc;
+        c->graph_comm = false;                  // as in enqueue: this RCCL build does not capture
+        c->err[0] = 0;
+    }
+    return 0;
+}
+
 int lpg_sync(lpg_ctx *c, lpg_result *out) {
     if (!c) return fail(c, LPG_ERR_ARG, "ctx is NULL");
     int rc;

@@ -219,6 +219,10 @@ class Engine:
     def reserve_log(self, n: int):
         self._check(self.lib.lpg_reserve_log(self._ctx, n), "lpg_reserve_log")
 
+    def prepare(self, rule: int = L.RULE_DANTZIG):
+        """Build the replayed pivot graph now (no pivots run; include/lpg.h lpg_prepare)."""
+        self._check(self.lib.lpg_prepare(self._ctx, rule), "lpg_prepare")
+
     def device_sync(self):
         self._check(self.lib.lpg_device_sync(self._ctx), "lpg_device_sync")
 

@@ -272,6 +272,32 @@ def test_graph_replay_identical(lpg, defer, monkeypatch):
     _assert_same(f, o, m)
 
 
+@pytest.mark.parametrize("defer", ["0", "32", "64"])
+def test_prepare_then_replay(lpg, defer, monkeypatch):
+    """lpg_prepare builds the replayed graph ahead of time (here after an odd
+    number of pivots, with a block open); the pivots that follow replay it and
+    stay bitwise on the oracle's path, and a prepare under the other rule is a
+    rebuild, not an error."""
+    monkeypatch.setenv("LPG_DEFER", defer)
+    m, n = 200, 300
+    e = lpg.Engine(m, n + m + 1)
+    o = Oracle(m, n + m + 1)
+    e.generate(n, 62, 0)
+    o.generate(n, 62, 0)
+    e.enqueue(3, 0)
+    e.prepare(0)
+    e.prepare(0)               # already built: no-op
+    e.enqueue(200, 0)
+    r = e.sync()
+    o.solve(203, 0)
+    assert r.pivots == o.get_log()[0].size
+    _assert_same(e, o, m)
+    e.prepare(1)
+    res, ores = e.solve(100_000, 1), o.solve(100_000, 1)
+    assert res.status == ores.status and res.pivots == ores.pivots
+    _assert_same(e, o, m)
+
+
 def test_timing_counters(lpg, monkeypatch):
     monkeypatch.setenv("LPG_DEFER", "0")
     e = lpg.Engine(512, 512 + 1024 + 1)
