@@ -1179,13 +1179,17 @@ int launch_prep_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s,
 #define LPG_PM(R, PF)                                                                                                 \
     hipLaunchKernelGGL((k_prep_d<R, PF, 256, true>), dim3(npp_d), dim3(256), 0, stream, g.T, g, st, s, cand, ncand, P, \
                        Cs, nullptr, D)
-    const bool wide = D.q >= 32;
+    const int pf = D.q < 16 ? 16 : D.q < 32 ? 32 : D.q < 48 ? 48 : 64;   // as launch_pivot_d
     if (rule == RULE_BLAND) {
-        if (wide) LPG_PM(RULE_BLAND, 64);
-        else LPG_PM(RULE_BLAND, 32);
+        if (pf == 16) LPG_PM(RULE_BLAND, 16);
+        else if (pf == 32) LPG_PM(RULE_BLAND, 32);
+        else if (pf == 48) LPG_PM(RULE_BLAND, 48);
+        else LPG_PM(RULE_BLAND, 64);
     } else {
-        if (wide) LPG_PM(RULE_DANTZIG, 64);
-        else LPG_PM(RULE_DANTZIG, 32);
+        if (pf == 16) LPG_PM(RULE_DANTZIG, 16);
+        else if (pf == 32) LPG_PM(RULE_DANTZIG, 32);
+        else if (pf == 48) LPG_PM(RULE_DANTZIG, 48);
+        else LPG_PM(RULE_DANTZIG, 64);
     }
 #undef LPG_PM
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1201,13 +1205,17 @@ int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int 
 #define LPG_SM(R, PF)                                                                                               \
     hipLaunchKernelGGL((k_select_d<R, PF, 256>), dim3(nsel), dim3(256), 0, stream, g.T, g, st, s, s1, Cs, Cs1, pp, \
                        npp, basis, part, D)
-    const bool wide = D.q >= 32;
+    const int pf = D.q < 16 ? 16 : D.q < 32 ? 32 : D.q < 48 ? 48 : 64;   // as launch_pivot_d
     if (rule == RULE_BLAND) {
-        if (wide) LPG_SM(RULE_BLAND, 64);
-        else LPG_SM(RULE_BLAND, 32);
+        if (pf == 16) LPG_SM(RULE_BLAND, 16);
+        else if (pf == 32) LPG_SM(RULE_BLAND, 32);
+        else if (pf == 48) LPG_SM(RULE_BLAND, 48);
+        else LPG_SM(RULE_BLAND, 64);
     } else {
-        if (wide) LPG_SM(RULE_DANTZIG, 64);
-        else LPG_SM(RULE_DANTZIG, 32);
+        if (pf == 16) LPG_SM(RULE_DANTZIG, 16);
+        else if (pf == 32) LPG_SM(RULE_DANTZIG, 32);
+        else if (pf == 48) LPG_SM(RULE_DANTZIG, 48);
+        else LPG_SM(RULE_DANTZIG, 64);
     }
 #undef LPG_SM
     return hipGetLastError() == hipSuccess ? 0 : -1;
