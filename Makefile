@@ -11,7 +11,7 @@ LIB       = linearprogramming_amd/liblpg.so
 all: $(LIB) host/lpgcli oracle
 
 $(LIB): $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h include/lpg.h
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_ctx.hip -lrccl
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_ctx.hip -ldl
 
 host/lpgcli: host/lpgcli.c include/lpg.h $(LIB)
 	$(CC) -O2 -std=c11 -Wall -Wextra -Iinclude -o $@ host/lpgcli.c -L$(dir $(LIB)) -llpg -Wl,-rpath,'$$ORIGIN/../linearprogramming_amd' -lm

@@ -2,13 +2,19 @@
 
 Workload (BASELINE.json `metric`, config 3): dense synthetic LP m=16384,
 n=32768 (tableau 16385 x 49153 fp64 = 6.44 GB), Dantzig pricing, generated on
-the device (splitmix64, seed 20220518). A "step" is one simplex pivot:
-price (argmin over the reduced-cost row) -> ratio test (min over the entering
-column) -> Gauss-Jordan rank-1 update of the whole tableau. By default the
-update is deferred: prep / select evaluate the pending chain for the entries
-they need and k_flushw applies each block of K pivots (LPG_DEFER; 64 for
-tableaus >= 512 MB per rank, else 32) to the constraint rows in one HBM pass,
-bitwise identical to K eager updates.
+the device (splitmix64, seed 20220518). Each simplex pivot is price (argmin
+over the reduced-cost row) -> ratio test (min over the entering column) ->
+Gauss-Jordan rank-1 update of the whole tableau. The update is deferred:
+prep / select evaluate the pending chain for the entries they need and
+k_flushw applies each block of K pivots (LPG_DEFER; 64 for tableaus >= 512 MB
+per rank, else 32) to the constraint rows in one HBM pass, bitwise identical
+to K eager updates.
+
+A "step" is one such block: K pivots and the one pass over the tableau that
+applies them (with --defer 0, eager updates, a step is one pivot). `value` is
+pivots/s = steps x K / time; `ms_per_step` is the time of one block. Warm-up
+steps are whole blocks too, so every timed pass applies exactly K pending
+pivots (the kernel and K named in `roofline`).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -35,10 +41,9 @@ import json
 import os
 import time
 
-import torch  # noqa: F401  (torch.distributed plumbing; imported first so one HIP runtime serves both)
-import torch.distributed as dist
-
-import linearprogramming_amd as lpg
+import linearprogramming_amd as lpg   # first: binds the process to the system ROCm runtime (_lib.bind_runtime)
+import torch  # noqa: E402  (torch.distributed gloo plumbing only; reuses that runtime)
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "Simplex pivots/sec + HBM GB/s fraction, dense m=16384×n=32768 fp64, 1/2/4/8 GPU"
@@ -56,8 +61,8 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=192)   # 3 whole deferred blocks of 64
-    ap.add_argument("--warmup", type=int, default=64)   # 1 block: page-in + the replayed hipGraph is built
+    ap.add_argument("--steps", type=int, default=16)    # deferred blocks (K pivots each) timed
+    ap.add_argument("--warmup", type=int, default=2)    # blocks before the timed region (page-in, graph build)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
@@ -158,8 +163,6 @@ def main():
         return config5(a)
     if a.variant is not None:
         os.environ["LPG_UPDATE_VARIANT"] = str(a.variant)
-    if a.defer is not None:
-        os.environ["LPG_DEFER"] = str(a.defer)
     if a.no_skip:
         os.environ["LPG_NO_SKIP"] = "1"
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -185,23 +188,25 @@ def main():
     elif a.force_rccl:
         eng.comm_init_rccl(lpg.Engine.rccl_unique_id())
     eng.generate(n, SEED, lpg.GEN_DENSE)
-    eng.reserve_log(a.warmup + a.steps + 8)
-    eng.enqueue(a.warmup, lpg.RULE_DANTZIG)
+    K = eng.info.defer_k or 1                           # pivots per step (one block; eager: one pivot)
+    warm, timed = a.warmup * K, a.steps * K
+    eng.reserve_log(warm + timed + 8)
+    eng.enqueue(warm, lpg.RULE_DANTZIG)
     before = eng.sync().pivots
 
-    # Per-pivot HIP events in the timed region (the roofline numerator's
-    # kernel time). For config 2 the events would forbid the hipGraph replay
-    # that hides its launch overhead, so config 2 times the update kernel in a
-    # second, event-instrumented pass right after the timed region.
+    # HIP events around the block pass inside the timed region (the roofline
+    # numerator's kernel time). For config 2 the events would forbid the
+    # hipGraph replay that hides its launch overhead, so config 2 times the
+    # pass in an event-instrumented run of 3 blocks before the timed region.
     live_events = a.config != 2
-    if not live_events:                                # config 2: event-instrumented pass first, while the LP
-        eng.set_timing(True)                           # is far from optimal, then the graph-replayed timed region
+    if not live_events:
+        eng.set_timing(True)
         eng.get_timing()
-        eng.enqueue(96, lpg.RULE_DANTZIG)
+        eng.enqueue(3 * K, lpg.RULE_DANTZIG)
         eng.sync()
         timing = eng.get_timing()
         eng.set_timing(False)
-        eng.enqueue(128, lpg.RULE_DANTZIG)             # builds the replayed hipGraph outside the timed region
+        eng.enqueue(4 * K, lpg.RULE_DANTZIG)           # builds the replayed hipGraph outside the timed region
         before = eng.sync().pivots
     eng.set_timing(live_events)
     if live_events:
@@ -211,7 +216,7 @@ def main():
         dist.barrier()
     eng.device_sync()
     t0 = time.perf_counter()
-    eng.enqueue(a.steps, lpg.RULE_DANTZIG)
+    eng.enqueue(timed, lpg.RULE_DANTZIG)
     res = eng.sync()
     eng.device_sync()
     t1 = time.perf_counter()
@@ -232,13 +237,41 @@ def main():
         dist.all_reduce(dd, op=dist.ReduceOp.MIN)
         done = int(dd.item())
     upd_ms = timing.update_ms / max(timing.update_count, 1)
-    # bytes the update / flush kernel actually read + wrote (columns whose
-    # pending P entries are all zero are not counted); in
-    # deferred mode the events bracket the block pass alone (k_flushw /
-    # k_flushm), so this agrees with rocprofv3's average for that kernel
+    # bytes the block pass actually read + wrote (columns whose K pending P
+    # entries are all zero are not counted, SURVEY.md §8(d) restated per block
+    # in DESIGN.md §6); the events bracket the pass alone, so this agrees with
+    # rocprofv3's average for that kernel
     touched = timing.update_bytes / max(timing.update_count, 1)
-    defer = eng.info.defer_k
+    defer = info.defer_k
     achieved = touched / (upd_ms * 1e-3) / 1e9 if upd_ms > 0 else 0.0
+    kname = ("k_flushw" if lpg.flush_kernel_for(defer) == "w" else "k_flushm") if defer else "k_update"
+    ms_block = elapsed * 1e3 / max(done, 1) * K
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "kernel": f"lpg::{kname}" + (f" (Gauss-Jordan block pass, {defer} pending pivots per launch; HIP events "
+                                         f"around this kernel alone)" if defer else " (Gauss-Jordan rank-1)"),
+            "pending_pivots_per_launch": defer or 1,
+            "launches_timed": timing.update_count,
+            "algorithmic_bytes_per_launch": touched,
+            "full_tableau_bytes_per_launch": info.bytes_per_pivot,
+            "column_skipping": not a.no_skip,
+            "update_ms_mean": upd_ms}
+    if defer and live_events:
+        # per-block ceiling: the pass at the HBM spec peak plus the measured rest of the block (pivot kernels,
+        # column trade, pivot-row rewrite, launch gaps), i.e. what this design reaches with a perfect pass
+        other_ms = ms_block - upd_ms
+        ceil_ms = touched / (HBM_PEAK_GBS * 1e9) * 1e3 + other_ms
+        roof.update({"ms_per_block": ms_block, "other_ms_per_block": other_ms,
+                     "block_ceiling_ms": ceil_ms, "block_ceiling_pivots_per_s": defer / (ceil_ms * 1e-3),
+                     "pass_only_ceiling_pivots_per_s": defer / (touched / (HBM_PEAK_GBS * 1e9))})
+    pmc = os.path.join(ROOT, "profiles", f"pmc_config{a.config}.json")
+    if os.path.exists(pmc) and defer:
+        with open(pmc) as f:
+            p = json.load(f)
+        if p.get("kernel") == kname and p.get("pending_pivots") == defer and world == 1:
+            roof["traffic"] = p.get("hbm_bytes_per_launch")
+            roof["traffic_source"] = (f"static: {os.path.relpath(pmc, ROOT)} (separate rocprofv3 --pmc passes of this "
+                                      f"bench, {kname}, {defer} pending pivots)")
     line = {
         "metric": METRIC,
         "value": done / elapsed,
@@ -246,7 +279,7 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": elapsed / max(done, 1) * 1e3,
+        "ms_per_step": ms_block,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -254,33 +287,18 @@ def main():
         "data": f"synthetic dense LP generated on device (splitmix64 seed {SEED}): A_ij=u, b_i=n/8(1+u), c_j=1+u",
         "config": {"workload": cfg["name"], "m": m, "n": n, "tableau": [m + 1, n + m + 1],
                    "tableau_GB": (m + 1) * (n + m + 1) * 8 / 1e9, "rule": "dantzig",
+                   "step": (f"one deferred block: {K} pivots + one block pass" if defer else "one pivot (eager)"),
+                   "pivots_timed": done,
                    "parallelism": f"row-block x{world}" + (" (RCCL allgather + allreduce per pivot)"
                                                            if world > 1 or a.force_rccl else ""),
                    "update": (f"deferred blocks of {defer} pivots (one k_flush pass per block)" if defer
                               else "eager rank-1 update per pivot"),
                    "update_variant": int(os.environ.get("LPG_UPDATE_VARIANT", "-1"))},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": (f"lpg::{'k_flushw' if defer > 32 else 'k_flushm'} (Gauss-Jordan, {defer} pending "
-                                f"pivots per pass; HIP events around this kernel alone)" if defer
-                                else "lpg::k_update (Gauss-Jordan rank-1)"),
-                     "launches_timed": timing.update_count,
-                     "algorithmic_bytes_per_launch": touched,
-                     "full_tableau_bytes_per_launch": info.bytes_per_pivot,
-                     "column_skipping": not a.no_skip,
-                     "update_ms_mean": upd_ms,
-                     "other_ms_per_pivot": ((elapsed * 1e3 - timing.update_ms) / max(done, 1) if live_events and defer
-                                            else timing.select_ms / max(done if live_events else 96, 1))},
+        "roofline": roof,
         "status": lpg.STATUS_NAMES.get(res.status, res.status),
         "pivots_total": res.pivots,
         "objective": res.objective,
     }
-    pmc = os.path.join(ROOT, "profiles", f"pmc_config{a.config}.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            p = json.load(f)
-        line["roofline"]["traffic"] = p.get("hbm_bytes_per_launch")
-        line["roofline"]["traffic_source"] = os.path.relpath(pmc, ROOT)
     if world == 1 and rank == 0 and not a.no_cpu:
         log = eng.get_log()
         eng.close()

@@ -6,7 +6,10 @@ and __graft_entry__.py. See DESIGN.md.
 """
 from ._lib import (GEN_ARTIFICIAL, GEN_DEGENERATE, GEN_DENSE, GEN_DUAL, ITER_LIMIT, NUMERIC, OPTIMAL, RULE_BLAND, RULE_DANTZIG, RUNNING,
                    STATUS_NAMES, UNBOUNDED, LIB_PATH, load)
-from .engine import Engine, LPGError, SolveResult, device_count
+from ._lib import bind_runtime, mapped_runtimes
+from .engine import Engine, LPGError, SolveResult, device_count, flush_kernel_for
 
-__all__ = ["Engine", "LPGError", "SolveResult", "device_count", "load", "LIB_PATH", "RULE_DANTZIG", "RULE_BLAND",
+bind_runtime()   # one HIP runtime per process, whatever is imported next (see _lib.bind_runtime)
+
+__all__ = ["bind_runtime", "mapped_runtimes", "Engine", "LPGError", "SolveResult", "device_count", "flush_kernel_for", "load", "LIB_PATH", "RULE_DANTZIG", "RULE_BLAND",
            "GEN_DENSE", "GEN_DEGENERATE", "GEN_ARTIFICIAL", "GEN_DUAL", "RUNNING", "OPTIMAL", "UNBOUNDED", "ITER_LIMIT", "NUMERIC", "STATUS_NAMES"]

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblpg.so")
@@ -96,6 +97,79 @@ PROTOTYPES = [
 ]
 
 _lib = None
+_runtime = None
+
+# The unversioned names under which torch's bundled ROCm libraries NEED the
+# runtime (torch/lib/libtorch_hip.so -> libamdhip64.so, librccl.so, ...).
+# Dependencies first; every one of these is also bundled in torch/lib. RCCL
+# (and the librocm_smi64 it pulls in) is deliberately absent: the system copy
+# next to torch aborts at exit, so liblpg opens RCCL only when a communicator
+# is attached, reusing torch's copy when torch is loaded (lpg_ctx.hip rccl_api).
+_RUNTIME_NAMES = ("libnuma.so", "libelf.so", "libdrm.so", "libdrm_amdgpu.so", "librocm-core.so", "libroctx64.so",
+                  "librocprofiler-register.so", "libamd_comgr.so", "libhsa-runtime64.so", "libamdhip64.so",
+                  "libhiprtc.so")
+
+
+def bind_runtime() -> str:
+    """Make the whole process use ONE HIP runtime, whatever is imported next.
+
+    liblpg.so NEEDs libamdhip64.so.7 (the system ROCm 7.2 the C host links);
+    torch's bundled libraries NEED the unversioned names (libamdhip64.so,
+    libhsa-runtime64.so, ...) and ship their own ROCm 7.0 copies. The dynamic loader reuses an already-loaded object when
+    the requested name equals its SONAME or a name it was opened under, so:
+
+    * torch already imported: liblpg's versioned NEEDED entry matches the
+      SONAME of torch's copy (libamdhip64.so.7) -> torch's runtime serves
+      both;
+    * otherwise: open the system ROCm libraries here under exactly the
+      unversioned names torch will ask for (resolved through ld.so.cache to
+      /opt/rocm), RTLD_GLOBAL; liblpg then binds to them by SONAME and a
+      later ``import torch`` binds to them by name -> one runtime, ROCm 7.2,
+      the one lpgcli and the bridged reference CLI use.
+
+    Before this, liblpg first and torch second mapped two libamdhip64 copies
+    and aborted at exit (profiles/r01_runtime_order.log). Returns "torch" or
+    "system"; tools/runtime_order.py checks /proc/self/maps for one copy of
+    each library.
+    """
+    global _runtime
+    if _runtime is not None:
+        return _runtime
+    if "torch" in sys.modules:
+        _runtime = "torch"
+        return _runtime
+    for name in _RUNTIME_NAMES:
+        try:
+            ctypes.CDLL(name, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:   # no system ROCm: liblpg's own NEEDED entries decide (and fail loudly if absent)
+            if name == "libamdhip64.so":
+                raise RuntimeError(f"system ROCm runtime not loadable ({e}); liblpg.so needs libamdhip64.so.7") from e
+    _runtime = "system"
+    return _runtime
+
+
+def mapped_runtimes() -> list:
+    """Paths of every libamdhip64 mapped into this process (diagnostic)."""
+    return sorted(p for p in mapped_libraries() if "libamdhip64" in p)
+
+
+def mapped_libraries() -> list:
+    """Real paths of every shared object mapped into this process."""
+    out = set()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            p = line.split()[-1]
+            if ".so" in p and p.startswith("/"):
+                out.add(os.path.realpath(p))
+    return sorted(out)
+
+
+def duplicated_libraries() -> dict:
+    """Library families mapped from more than one file (e.g. torch/lib and /opt/rocm copies)."""
+    fam = {}
+    for p in mapped_libraries():
+        fam.setdefault(os.path.basename(p).split(".so")[0], []).append(p)
+    return {k: v for k, v in fam.items() if len(v) > 1}
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -105,14 +179,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         return _lib
     if not os.path.exists(path):
         raise RuntimeError(f"lpg HIP engine not built: {path} is missing (run `make` or __graft_entry__.build())")
-    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same
-    # soname as /opt/rocm's). Loading torch first makes liblpg bind to the
-    # runtime torch will use; the reverse order (liblpg first, torch later)
-    # aborts at interpreter exit on the box (tools/runtime_order.py).
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    bind_runtime()
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, res, args in PROTOTYPES:
         fn = getattr(lib, name)

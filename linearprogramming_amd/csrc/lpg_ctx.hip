@@ -7,8 +7,9 @@
 // device and lpg_solve only synchronises every `batch` pivots to check the
 // device-side status (SURVEY.md §3 call stack (3)).
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
+#include <rccl/rccl.h>   // types only: RCCL itself is opened at the first communicator (rccl_api())
 
+#include <dlfcn.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -151,11 +152,47 @@ static int use_device(lpg_ctx *c) {
 
 static bool has_comm(const lpg_ctx *c) { return c->world > 1 || c->nccl || c->have_hops; }
 
+// RCCL is not a link-time dependency of liblpg.so. A process that already
+// holds an RCCL (torch's bundled librccl.so, SONAME librccl.so.1) keeps using
+// that one; otherwise the system ROCm's librccl.so.1 is opened here. Linking
+// it made every liblpg user map the system RCCL (and its librocm_smi64) at
+// load time, which aborted at exit next to torch's copies
+// (profiles/r01_runtime_order.log, linearprogramming_amd/_lib.py bind_runtime).
+struct RcclApi {
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *);
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int);
+    ncclResult_t (*CommDestroy)(ncclComm_t);
+    ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+    ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+    const char *(*GetErrorString)(ncclResult_t);
+};
+
+static const RcclApi *rccl_api() {
+    static RcclApi api;
+    static int state = 0;   // 0 untried, 1 ok, -1 unavailable
+    if (state) return state > 0 ? &api : nullptr;
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    state = -1;
+    if (!h) return nullptr;
+    api.GetUniqueId = (decltype(api.GetUniqueId))dlsym(h, "ncclGetUniqueId");
+    api.CommInitRank = (decltype(api.CommInitRank))dlsym(h, "ncclCommInitRank");
+    api.CommDestroy = (decltype(api.CommDestroy))dlsym(h, "ncclCommDestroy");
+    api.AllGather = (decltype(api.AllGather))dlsym(h, "ncclAllGather");
+    api.AllReduce = (decltype(api.AllReduce))dlsym(h, "ncclAllReduce");
+    api.GetErrorString = (decltype(api.GetErrorString))dlsym(h, "ncclGetErrorString");
+    if (api.GetUniqueId && api.CommInitRank && api.CommDestroy && api.AllGather && api.AllReduce && api.GetErrorString)
+        state = 1;
+    return state > 0 ? &api : nullptr;
+}
+
 static int comm_allgather(lpg_ctx *c, const void *send, void *recv, size_t bytes) {
     if (!has_comm(c)) return 0;
     if (c->nccl) {
-        ncclResult_t r = ncclAllGather(send, recv, bytes, ncclUint8, c->nccl, c->stream);
-        if (r != ncclSuccess) return fail(c, LPG_ERR_COMM, "ncclAllGather: %s", ncclGetErrorString(r));
+        const RcclApi *R = rccl_api();
+        ncclResult_t r = R->AllGather(send, recv, bytes, ncclUint8, c->nccl, c->stream);
+        if (r != ncclSuccess) return fail(c, LPG_ERR_COMM, "ncclAllGather: %s", R->GetErrorString(r));
         return 0;
     }
     if (!c->have_hops) return fail(c, LPG_ERR_STATE, "world > 1 but no communicator attached");
@@ -173,8 +210,9 @@ static int comm_allgather(lpg_ctx *c, const void *send, void *recv, size_t bytes
 static int comm_allreduce_sum(lpg_ctx *c, double *buf, size_t count) {
     if (!has_comm(c)) return 0;
     if (c->nccl) {
-        ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, c->nccl, c->stream);
-        if (r != ncclSuccess) return fail(c, LPG_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+        const RcclApi *R = rccl_api();
+        ncclResult_t r = R->AllReduce(buf, buf, count, ncclFloat64, ncclSum, c->nccl, c->stream);
+        if (r != ncclSuccess) return fail(c, LPG_ERR_COMM, "ncclAllReduce: %s", R->GetErrorString(r));
         return 0;
     }
     if (!c->have_hops) return fail(c, LPG_ERR_STATE, "world > 1 but no communicator attached");
@@ -718,9 +756,11 @@ int lpg_create(lpg_ctx **out, int device, int64_t m, int64_t ncols, uint32_t fla
 
 int lpg_comm_unique_id(void *uid, size_t len) {
     if (!uid || len < sizeof(ncclUniqueId)) return fail(nullptr, LPG_ERR_ARG, "uid buffer too small");
+    const RcclApi *R = rccl_api();
+    if (!R) return fail(nullptr, LPG_ERR_COMM, "RCCL (librccl.so.1) not loadable");
     ncclUniqueId id;
-    ncclResult_t r = ncclGetUniqueId(&id);
-    if (r != ncclSuccess) return fail(nullptr, LPG_ERR_COMM, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+    ncclResult_t r = R->GetUniqueId(&id);
+    if (r != ncclSuccess) return fail(nullptr, LPG_ERR_COMM, "ncclGetUniqueId: %s", R->GetErrorString(r));
     memcpy(uid, &id, sizeof id);
     return 0;
 }
@@ -739,15 +779,17 @@ static void comm_pivot_blocks(lpg_ctx *c) {
 int lpg_comm_init_rccl(lpg_ctx *c, const void *uid, size_t len) {
     if (!c || !uid || len < sizeof(ncclUniqueId)) return fail(c, LPG_ERR_ARG, "bad uid");
     if (c->nccl || c->have_hops) return fail(c, LPG_ERR_STATE, "communicator already attached");
+    const RcclApi *R = rccl_api();
+    if (!R) return fail(c, LPG_ERR_COMM, "RCCL (librccl.so.1) not loadable");
     int rc;
     if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;   // the generic kernels work in caller order
     ncclUniqueId id;
     memcpy(&id, uid, sizeof id);
     comm_pivot_blocks(c);
-    ncclResult_t r = ncclCommInitRank(&c->nccl, c->world, id, c->rank);
+    ncclResult_t r = R->CommInitRank(&c->nccl, c->world, id, c->rank);
     if (r != ncclSuccess) {
         c->nccl = nullptr;
-        return fail(c, LPG_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
+        return fail(c, LPG_ERR_COMM, "ncclCommInitRank: %s", R->GetErrorString(r));
     }
     return 0;
 }
@@ -768,7 +810,7 @@ void lpg_destroy(lpg_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     graph_drop(c);
-    if (c->nccl) ncclCommDestroy(c->nccl);
+    if (c->nccl) rccl_api()->CommDestroy(c->nccl);
     for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
@@ -801,6 +843,9 @@ int lpg_load_rows(lpg_ctx *c, int64_t row0, int64_t nrows, const double *rows, i
         return fail(c, LPG_ERR_ARG, "lpg_load_rows: bad arguments");
     int rc;
     if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;
+    // canonicalize() queues work on c->stream (non-blocking): the synchronous
+    // copies below go through the null stream and must not overtake it
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     // constraint rows inside this rank's block
     const int64_t a = std::max(row0, c->row0), b = std::min(row0 + nrows, c->row0 + c->nloc);
     if (a < b)

@@ -55,6 +55,13 @@ def _stdout_to_stderr():
         os.close(saved)
 
 
+def flush_kernel_for(pending: int) -> str:
+    """Which block-pass kernel the default configuration launches for `pending`
+    pivots (lpg_kernels.hip launch_flush_main): "w" = k_flushw (a 64-slot
+    block), "m" = k_flushm (<= 32 slots)."""
+    return "w" if pending > 32 else "m"
+
+
 def device_count() -> int:
     lib = L.load()
     n = ctypes.c_int(0)

@@ -8,7 +8,7 @@ set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 CFG=${CFG:-3}
-STEPS=${STEPS:-128}  # whole deferred blocks (2 x 64), no warm-up: every flush applies a full block
+STEPS=${STEPS:-2}   # whole deferred blocks (bench.py steps), no warm-up: every flush applies a full block
 mkdir -p $OUT
 echo "[profile] trace" >&2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
