@@ -1,0 +1,156 @@
+"""Parity at BASELINE.json's full sizes (configs 3, 4 and 5), on the device.
+
+* config 3 (16384 x 32768): 200 pivots = three whole deferred blocks of 64
+  (each ending in the column trade k_swap_plan / k_move_cols / k_fill_cols,
+  the block pass k_flushw over reordered columns and the pivot-row rewrite
+  k_flush_pivot_rows) plus 8 pending pivots flushed by the readout; bitwise
+  against the C oracle: pivot log, basis, column 0, objective row, every pivot
+  row and 64 sampled rows; basic columns are unit vectors on those rows.
+* config 5 (two-phase, Bland, m = n = 8192, KM-style degenerate with
+  equality rows): the whole solve to optimality, bitwise against the oracle
+  (status, pivot count, objective, log, basis, sampled rows).
+* config 4 (65536 x 131072, 103 GB tableau, one GPU): 192 pivots (three
+  blocks); the oracle cannot hold it, so size-independent properties over the
+  WHOLE tableau, read back in row chunks: every basic column is a unit vector
+  in every row, b >= 0 (primal feasibility), z is nondecreasing block to block,
+  and the objective row equals c_B T - c (recomputed on the host in global row
+  order on ~64 sampled columns and on column 0) to 1e-9 relative to
+  sum |c_B| |T| -- the device row is the result of 192 rank-1 updates, not of
+  that dot product, so this one is a tolerance, not bitwise.
+
+Reference: the pivot loop simplex.c:40 -> :65 lacks.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from oracle.lpo import Oracle
+
+pytestmark = pytest.mark.gpu
+SEED = 20220518
+
+
+@pytest.fixture(scope="module")
+def lpg():
+    import linearprogramming_amd as lpg
+    lpg.load()
+    assert lpg.device_count() >= 1, "no GPU visible"
+    return lpg
+
+
+def _oracle(m, ncols):
+    return Oracle(m, ncols, nthreads=min(16, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+
+
+def _log(x):
+    k, r = x.get_log()
+    return list(zip(k.tolist(), r.tolist()))
+
+
+def test_config3_three_blocks_bitwise(lpg):
+    m, n = 16384, 32768
+    e = lpg.Engine(m, n + m + 1)
+    assert e.info.defer_k == 64
+    e.generate(n, SEED, lpg.GEN_DENSE)
+    e.reserve_log(256)
+    e.enqueue(64, lpg.RULE_DANTZIG)          # block 1 (the replayed graph is built after it)
+    e.prepare(lpg.RULE_DANTZIG)
+    e.enqueue(128, lpg.RULE_DANTZIG)         # blocks 2 and 3, replayed
+    mid = e.sync()
+    assert mid.pivots == 192
+    res = e.solve(8, lpg.RULE_DANTZIG)       # 8 more: a partial block, flushed by the readout
+    assert res.status_name == "ITER_LIMIT" and res.pivots == 200
+    o = _oracle(m, n + m + 1)
+    o.generate(n, SEED, 0)
+    ores = o.solve(200, 0)
+    assert ores.pivots == 200 and res.objective == ores.objective
+    log = _log(e)
+    assert log == _log(o)
+    basis = e.get_basis()
+    assert np.array_equal(basis, o.get_basis())
+    rng = np.random.default_rng(3)
+    rows = sorted(set(rng.choice(m, 64, replace=False).tolist()) | {r for _, r in log} | {0, m - 1})
+    for i in rows:
+        ri = e.get_rows(i, 1)
+        assert np.array_equal(ri, o.get_rows(i, 1)), f"row {i}"
+        assert ri[0, basis[i]] == 1.0 and np.count_nonzero(ri[0, basis]) == 1, f"row {i} basic columns"
+    assert np.array_equal(e.get_rows(m, 1), o.get_rows(m, 1)), "objective row"
+    x0 = e.get_column0()
+    for i in rows:
+        assert x0[i] == o.get_rows(i, 1)[0, 0]
+
+
+def test_config5_two_phase_full_bitwise(lpg):
+    m = n = 8192
+    art_first = 1 + n + (m + 1) // 2
+    cap = 20000
+    e = lpg.Engine(m, n + m + 1)
+    e.generate(n, SEED, lpg.GEN_ARTIFICIAL)
+    e.reserve_log(cap + 8)
+    res = e.solve_two_phase(art_first, None, cap, lpg.RULE_BLAND)
+    o = _oracle(m, n + m + 1)
+    o.generate(n, SEED, 2)
+    ores = o.solve_two_phase(art_first, None, cap, lpg.RULE_BLAND)
+    assert res.status_name == "OPTIMAL" and res.status == ores.status
+    assert res.pivots == ores.pivots and res.pivots > 4096
+    assert res.objective == ores.objective
+    assert _log(e) == _log(o)
+    assert np.array_equal(e.get_basis(), o.get_basis())
+    rng = np.random.default_rng(5)
+    for i in sorted(set(rng.choice(m, 64, replace=False).tolist()) | {0, m - 1, m}):
+        assert np.array_equal(e.get_rows(i, 1), o.get_rows(i, 1)), f"row {i}"
+
+
+def test_config4_full_size_properties(lpg):
+    m, n = 65536, 131072
+    N1 = n + m + 1
+    e = lpg.Engine(m, N1)
+    assert e.info.defer_k == 64
+    e.generate(n, SEED, lpg.GEN_DENSE)
+    c = -e.get_rows(m, 1)[0, 1:]                # slack basis: row m = [0 | -c]
+    assert np.all(c[:n] > 0) and np.all(c[n:] == 0)
+    e.reserve_log(256)
+    zs = [0.0]
+    for _ in range(3):
+        r = e.solve(64, lpg.RULE_DANTZIG)
+        assert r.status_name == "ITER_LIMIT"
+        zs.append(r.objective)
+    assert r.pivots == 192
+    assert all(b >= a for a, b in zip(zs, zs[1:])) and zs[-1] > 0
+    basis = e.get_basis()
+    assert len(set(basis.tolist())) == m
+    log = _log(e)
+    entered = {k for k, _ in log}
+    obj = e.get_rows(m, 1)[0]
+    rng = np.random.default_rng(7)
+    nonbasic = np.setdiff1d(np.arange(1, N1), basis)
+    cols = np.unique(np.concatenate([[0], rng.choice(nonbasic, 56, replace=False),
+                                     np.array(sorted(entered))[:8]]))
+    cb = np.where(basis <= n, c[basis - 1], 0.0)       # costs of the basic variables (slacks: 0)
+    acc = np.zeros(len(cols))
+    scale = np.zeros(len(cols))
+    chunk = 256
+    for i0 in range(0, m, chunk):
+        blk = e.get_rows(i0, chunk)
+        # basic columns are unit vectors in every row
+        sub = blk[:, basis]
+        idx = np.arange(i0, i0 + chunk)
+        assert np.array_equal(sub[np.arange(chunk), idx], np.ones(chunk)), f"rows {i0}.."
+        assert np.count_nonzero(sub) == chunk, f"rows {i0}.. basic columns not unit"
+        assert np.all(blk[:, 0] >= 0.0), f"rows {i0}.. infeasible b"
+        t = blk[:, cols]
+        w = cb[i0:i0 + chunk]
+        for q in np.nonzero(w)[0]:               # c_B T in global row order
+            acc += w[q] * t[q]
+        scale += np.abs(w) @ np.abs(t)
+    d = acc.copy()
+    d[1:] -= np.where(cols[1:] <= n, c[np.maximum(cols[1:], 1) - 1], 0.0)
+    dev = obj[cols]
+    tol = 1e-9 * (scale + 1.0)
+    assert np.all(np.abs(d - dev) <= tol), np.max(np.abs(d - dev) / tol)
+    assert abs(obj[0] - zs[-1]) <= 1e-9 * abs(zs[-1])
+    # the entered columns are basic now: their reduced costs are exactly 0 in the device row
+    assert np.all(obj[basis] == 0.0)
