@@ -66,15 +66,18 @@ def parse():
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
-    ap.add_argument("--variant", type=int, default=None, help="update-kernel variant (LPG_UPDATE_VARIANT)")
+    ap.add_argument("--cpu-1core-seconds", type=float, default=6.0, help="1-core CPU baseline time budget")
+    ap.add_argument("--variant", type=int, default=None, help="eager update-kernel form (LPG_UPDATE_VARIANT 0|1)")
     ap.add_argument("--no-skip", action="store_true", help="update every column (disable column skipping)")
     ap.add_argument("--force-rccl", action="store_true", help="attach a 1-rank RCCL communicator at N=1 (times the exchange)")
     ap.add_argument("--defer", type=int, default=None, help="pivots per deferred block (LPG_DEFER; 0 = eager updates)")
     return ap.parse_args()
 
 
-def cpu_baseline(m, n, gpu_log, budget_s):
-    """Oracle leg: same LP, same rules, OpenMP on the host cores (rank 0, N=1 only)."""
+def cpu_baseline(m, n, gpu_log, budget_s, budget_1core_s):
+    """Oracle leg: same LP, same rules, OpenMP on the host cores (rank 0, N=1
+    only), then the same oracle on ONE core for a few more pivots of the same
+    solve (BASELINE.md CPU-baseline plan)."""
     from oracle.lpo import GEN_DENSE, RULE_DANTZIG, Oracle
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     o = Oracle(m, n + m + 1, nthreads=threads)
@@ -89,11 +92,22 @@ def cpu_baseline(m, n, gpu_log, budget_s):
     k, r = o.get_log()
     n_cmp = min(len(k), len(gpu_log[0]))
     same = bool((k[:n_cmp] == gpu_log[0][:n_cmp]).all() and (r[:n_cmp] == gpu_log[1][:n_cmp]).all())
+    one = None
+    if budget_1core_s > 0:
+        o.set_threads(1)
+        t1 = time.perf_counter()
+        d1 = 0
+        while d1 < 2 or (time.perf_counter() - t1 < budget_1core_s and d1 < 50):
+            o.solve(1, RULE_DANTZIG)
+            d1 += 1
+        s1 = time.perf_counter() - t1
+        one = {"value": d1 / s1, "unit": "pivots/s", "cores": 1, "kind": "port", "pivots": d1, "seconds": s1,
+               "sample": f"pivots {done + 2}..{done + 1 + d1} of the same solve, oracle/liblpo.so on 1 thread"}
     o.close()
     return {"value": done / dt, "unit": "pivots/s", "cores": threads, "kind": "port",
             "sample": f"{done} timed pivots (after 1 untimed) of the same {m}x{n} LP, oracle/liblpo.so "
                       f"(C fp64, OpenMP {threads} threads)",
-            "seconds": dt}, {"pivots_compared": int(n_cmp), "identical_pivot_sequence": same}
+            "seconds": dt, "single_core": one}, {"pivots_compared": int(n_cmp), "identical_pivot_sequence": same}
 
 
 def config5(a):
@@ -302,7 +316,7 @@ def main():
     if world == 1 and rank == 0 and not a.no_cpu:
         log = eng.get_log()
         eng.close()
-        cb, parity = cpu_baseline(m, n, log, a.cpu_seconds)
+        cb, parity = cpu_baseline(m, n, log, a.cpu_seconds, a.cpu_1core_seconds)
         line["cpu_baseline"] = cb
         line["parity"] = parity
     else:

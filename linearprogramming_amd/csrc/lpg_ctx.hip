@@ -72,7 +72,7 @@ struct lpg_ctx {
     // deferred (blocked) updates: defer_k pivots per flush (0 = eager)
     int defer_k = 0;
     int pend = 0;                 // pivots enqueued since the last flush (host view)
-    int flush_variant = 0;
+    int flush_variant = -1;       // launch_flush_main `which`: -1 default, 0 k_flushm, 1 k_flushw
     bool capture_block = false;   // capturing a deferred block's pivots (its flush stays outside the graph)
     bool fast_pivot = true;       // deferred single-rank pivots through k_prep_d / k_select_d (LPG_SLOW_PIVOT=1: generic pair)
     double *Pbuf = nullptr, *Cbuf = nullptr;
@@ -672,8 +672,8 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     }
     const char *sp = getenv("LPG_SLOW_PIVOT");
     c->fast_pivot = !(sp && atoi(sp));
-    const char *fv = getenv("LPG_FLUSH_VARIANT");
-    c->flush_variant = fv ? atoi(fv) : -1;   // -1: launch_flush default
+    const char *fv = getenv("LPG_FLUSH_KERNEL");   // m | w: force k_flushm / k_flushw (tests); default by block size
+    c->flush_variant = fv ? (fv[0] == 'w' ? 1 : fv[0] == 'm' ? 0 : -1) : -1;
     int rc;
     if ((rc = use_device(c))) { lpg_destroy(c); return rc; }
     const int64_t rows = c->nloc + c->nobj;

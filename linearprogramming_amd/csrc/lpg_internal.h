@@ -136,11 +136,11 @@ int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int 
                      double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part, int nsel,
                      const Defer &D);
 // Apply the pending pivots (st->npend <= kmax) to constraint rows 0..nloc-1.
-int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant);
+int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which);
 // ... in two parts: the block pass itself (k_flushw / k_flushm / k_flush), then
 // the pivot-row rewrite and the pending-counter reset (the rewrite's
 // multipliers come from launch_swap_plan, launched before either part)
-int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant);
+int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which);
 int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax);
 int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0: k too large)
 // Basis-partitioned column order (single-rank deferred path): after a block,

@@ -1557,49 +1557,28 @@ struct UpdateCfg {
     int persist;      // blocks per CU of a persistent grid; 0 = one block per item
 };
 
-// Variant table (LPG_UPDATE_VARIANT); every variant is bit-identical.
+// Two forms (LPG_UPDATE_VARIANT), bit-identical: 0 = one block per
+// (256-lane column tile x 64-row strip) item, 8 rows of loads in flight;
+// 1 = persistent grid (8 blocks per CU) with a dynamic dequeue, non-temporal
+// streaming and pipelined rows. (Round 1 swept 25 forms; these two were the
+// defaults.)
 static const UpdateCfg kUpdateCfgs[] = {
     {1, 8, false, false, 64, 0},    // 0
-    {2, 4, false, false, 64, 0},    // 1
-    {1, 8, true, false, 64, 0},     // 2  non-temporal
-    {2, 4, true, false, 64, 0},     // 3
-    {1, 4, false, false, 32, 0},    // 4
-    {4, 2, false, false, 64, 0},    // 5
-    {1, 8, false, false, 64, 8},    // 6  persistent, 8 blocks/CU
-    {1, 4, false, true, 64, 0},     // 7  pipelined
-    {1, 8, false, true, 64, 0},     // 8
-    {1, 4, false, true, 64, 8},     // 9  pipelined + persistent
-    {2, 4, false, true, 64, 0},     // 10
-    {1, 8, true, true, 64, 0},      // 11 pipelined + non-temporal
-    {1, 16, false, false, 128, 0},  // 12
-    {1, 4, false, true, 256, 4},    // 13 tall strips, persistent 4/CU
-    {1, 8, true, false, 64, 8},     // 14 persistent + non-temporal
-    {2, 4, true, false, 64, 8},     // 15 2 slices/lane, persistent + non-temporal
-    {1, 8, false, false, 64, 4},    // 16 persistent 4/CU
-    {1, 8, true, true, 64, 8},      // 17 persistent + non-temporal + pipelined
-    {1, 8, false, false, 32, 8},    // 18 persistent, 32-row strips
-    {1, 8, true, false, 32, 8},     // 19 persistent + non-temporal, 32-row strips
-    {1, 8, true, false, 64, 8},     // 20 persistent + non-temporal, dynamic dequeue
-    {1, 8, true, true, 64, 8},      // 21 persistent + non-temporal + pipelined, dynamic dequeue
-    {1, 8, false, false, 64, 8},    // 22 persistent, dynamic dequeue
-    {2, 4, true, false, 64, 8},     // 23 2 slices/lane, persistent + non-temporal, dynamic
-    {1, 8, true, false, 64, 4},     // 24 persistent 4/CU + non-temporal, dynamic
+    {1, 8, true, true, 64, 8},      // 1
 };
 constexpr int kNumUpdateCfgs = sizeof(kUpdateCfgs) / sizeof(kUpdateCfgs[0]);
 
 int update_variants() { return kNumUpdateCfgs; }
 
-// Default (variant < 0): large tableaus use the persistent grid with a
-// dynamic dequeue, non-temporal streaming and pipelined rows (variant 21:
+// Default (variant < 0): large tableaus use the persistent grid (variant 1:
 // steady at the read-modify-write ceiling when skipped columns make the work
 // per tile uneven; measured best from 2048 to 16385 rows); small ones (fewer
-// than 2048 work items, e.g. config 2, MALL-resident)
-// use one block per item (variant 0), where the dequeue atomics would cost
-// more than they balance.
+// than 2048 work items, e.g. config 2, MALL-resident) use one block per item
+// (variant 0), where the dequeue atomics would cost more than they balance.
 int update_auto_variant(const Geo &g) {
     const int64_t nvec = (g.ncols + 1) / 2;
     const int64_t items = ((nvec + kBlock - 1) / kBlock) * ((g.nloc + g.nobj + 63) / 64);
-    return items >= 2048 ? 21 : 0;
+    return items >= 2048 ? 1 : 0;
 }
 
 int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const double *P, const double *Cs,
@@ -1624,33 +1603,10 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
     hipLaunchKernelGGL((k_update<V, R, N, PI, D>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, ntiles, strip, \
                        nitems, basis, logk, logr, skip)
 #define LPG_UPD(V, R, N, PI) LPG_UPD_(V, R, N, PI, false)
-    switch (variant) {
-        case 1: LPG_UPD(2, 4, false, false); break;
-        case 2: LPG_UPD(1, 8, true, false); break;
-        case 3: LPG_UPD(2, 4, true, false); break;
-        case 4: LPG_UPD(1, 4, false, false); break;
-        case 5: LPG_UPD(4, 2, false, false); break;
-        case 6: LPG_UPD(1, 8, false, false); break;
-        case 7: LPG_UPD(1, 4, false, true); break;
-        case 8: LPG_UPD(1, 8, false, true); break;
-        case 9: LPG_UPD(1, 4, false, true); break;
-        case 10: LPG_UPD(2, 4, false, true); break;
-        case 11: LPG_UPD(1, 8, true, true); break;
-        case 12: LPG_UPD(1, 16, false, false); break;
-        case 13: LPG_UPD(1, 4, false, true); break;
-        case 14: LPG_UPD(1, 8, true, false); break;
-        case 15: LPG_UPD(2, 4, true, false); break;
-        case 16: LPG_UPD(1, 8, false, false); break;
-        case 17: LPG_UPD(1, 8, true, true); break;
-        case 18: LPG_UPD(1, 8, false, false); break;
-        case 19: LPG_UPD(1, 8, true, false); break;
-        case 20: LPG_UPD_(1, 8, true, false, true); break;
-        case 21: LPG_UPD_(1, 8, true, true, true); break;
-        case 22: LPG_UPD_(1, 8, false, false, true); break;
-        case 23: LPG_UPD_(2, 4, true, false, true); break;
-        case 24: LPG_UPD_(1, 8, true, false, true); break;
-        default: LPG_UPD(1, 8, false, false); break;
-    }
+    if (variant == 1)
+        LPG_UPD_(1, 8, true, true, true);
+    else
+        LPG_UPD(1, 8, false, false);
 #undef LPG_UPD
 #undef LPG_UPD_
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1659,131 +1615,14 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
 // ------------------------------------------------------------------------
 // flush (deferred mode, a12 blocked): apply the np pending pivots to the
 // constraint rows 0..nloc-1 in ONE read-modify-write pass over HBM instead
-// of np passes. Work item = (256-column tile, strip of SR rows). Each lane
-// owns one column j and keeps P_0[j] .. P_{np-1}[j] in VGPRs for the whole
-// strip; the multipliers C_q[i] are wave-uniform and come through the scalar
-// cache (Cbuf is column-major per pivot, so C_q[i..i+RU) is one scalar load).
-// Per element the np fma run in pending order — bit for bit what np eager
-// updates compute; the (at most np) pivot rows, whose chain restarts at
-// x = P_q[j], are rewritten by k_flush_pivot_rows right after. Columns whose
-// pending P entries are all zero are skipped (as in k_update). Persistent
-// grid, dynamic dequeue (st->fwork), RU rows of loads in flight per lane,
-// optionally pipelined.
+// of np passes. Per element the np fma run in pending order -- bit for bit
+// what np eager updates compute; the (at most np) pivot rows, whose chain
+// restarts at x = P_q[j], are rewritten by k_flush_pivot_rows right after.
+// Columns whose pending P entries are all zero are skipped (as in k_update).
+// Two kernels, both on the matrix cores: k_flushm (blocks of <= 32 pivots)
+// and k_flushw (64-pivot blocks). (Round 1 also carried VALU-fma and
+// one-column-per-lane MFMA forms, bitwise identical and slower; removed.)
 // ------------------------------------------------------------------------
-
-template <int RU, bool NT>
-__device__ __forceinline__ void fl_load(double (&x)[RU], const double *col, int64_t i, int64_t ld, bool ok) {
-#pragma unroll
-    for (int u = 0; u < RU; u++) {
-        const double *a = col + (i + u) * ld;
-        x[u] = ok ? (NT ? __builtin_nontemporal_load(a) : *a) : 0.0;
-    }
-}
-
-template <int RU, bool NT>
-__device__ __forceinline__ void fl_store(const double (&x)[RU], double *col, int64_t i, int64_t ld, bool ok) {
-    if (!ok) return;
-#pragma unroll
-    for (int u = 0; u < RU; u++) {
-        double *a = col + (i + u) * ld;
-        if (NT) __builtin_nontemporal_store(x[u], a);
-        else *a = x[u];
-    }
-}
-
-// The pending chain on RU consecutive rows (pivot rows are rewritten
-// afterwards by k_flush_pivot_rows). sC holds the strip's multipliers,
-// [slot][row], zero for slots >= np (with p[q] == 0 there, fma(-0, 0, x) == x
-// bit for bit, signed zeros and NaN included), so the loop is straight-line.
-// The reads are LDS broadcasts (every lane the same address).
-template <int KMAX, int RU, int SR>
-__device__ __forceinline__ void fl_chain(double (&x)[RU], const double (&p)[KMAX], const double *sC, int lr) {
-#pragma unroll
-    for (int q = 0; q < KMAX; q++) {
-        double c[RU];
-#pragma unroll
-        for (int u = 0; u < RU; u++) c[u] = sC[q * SR + lr + u];
-#pragma unroll
-        for (int u = 0; u < RU; u++) x[u] = fma(-c[u], p[q], x[u]);
-    }
-}
-
-template <int KMAX, int RU, bool NT, bool PIPE, int SR>
-__global__ __launch_bounds__(kBlock) void k_flush(double *__restrict__ T, Geo g, DevState *__restrict__ st,
-                                                  const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
-                                                  int64_t cs, int64_t ntiles, int64_t nitems, int skip) {
-    const int np = (int)st->npend;
-    if (np <= 0) return;
-    const int64_t ld = g.ld;
-    unsigned long long touched = 0;
-    __shared__ int64_t next_item;
-    __shared__ __attribute__((aligned(16))) double sC[KMAX * SR];
-    for (;;) {
-        __syncthreads();
-        if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
-        __syncthreads();
-        const int64_t item = next_item;
-        if (item >= nitems) break;
-        const int64_t tile = item % ntiles, strip = item / ntiles;
-        const int64_t i0 = strip * SR;
-        const int64_t i1 = i0 + SR < g.nloc ? i0 + SR : g.nloc;
-        const int64_t j = tile * kBlock + threadIdx.x;
-        bool ok = j < g.ncols;
-        double p[KMAX];
-        bool live = false;
-#pragma unroll
-        for (int q = 0; q < KMAX; q++) {
-            p[q] = (q < np && ok) ? Pbuf[(int64_t)q * ld + j] : 0.0;
-            live = live || p[q] != 0.0;
-        }
-        if (skip) ok = ok && live;   // all pending P zero: the column keeps its values
-        const int cnt = __syncthreads_count(ok);
-        if (cnt == 0) continue;
-        if (threadIdx.x == 0) touched += (unsigned long long)cnt * (unsigned long long)(i1 - i0);
-        // stage C_q[i0 .. i0 + SR) for every slot (zeros past np)
-        for (int e = threadIdx.x; e < KMAX * SR / 2; e += kBlock) {
-            const int q = e / (SR / 2), rr = 2 * (e % (SR / 2));
-            d2 v = d2{0.0, 0.0};
-            if (q < np && i0 + rr < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + i0 + rr);   // i0 + rr + 1 < cs
-            *(d2 *)(sC + q * SR + rr) = v;
-        }
-        __syncthreads();
-        double *col = T + j;
-        int lr = 0;
-        const int nr = (int)(i1 - i0);
-        if (PIPE) {
-            if (lr + RU <= nr) {
-                double x[RU];
-                fl_load<RU, NT>(x, col, i0 + lr, ld, ok);
-                for (;;) {
-                    const bool more = lr + 2 * RU <= nr;
-                    double nx[RU];
-                    if (more) fl_load<RU, NT>(nx, col, i0 + lr + RU, ld, ok);
-                    fl_chain<KMAX, RU, SR>(x, p, sC, lr);
-                    fl_store<RU, NT>(x, col, i0 + lr, ld, ok);
-                    lr += RU;
-                    if (!more) break;
-#pragma unroll
-                    for (int u = 0; u < RU; u++) x[u] = nx[u];
-                }
-            }
-        } else {
-            for (; lr + RU <= nr; lr += RU) {
-                double x[RU];
-                fl_load<RU, NT>(x, col, i0 + lr, ld, ok);
-                fl_chain<KMAX, RU, SR>(x, p, sC, lr);
-                fl_store<RU, NT>(x, col, i0 + lr, ld, ok);
-            }
-        }
-        for (; lr < nr; lr++) {      // tail rows of the last strip
-            double x[1];
-            fl_load<1, NT>(x, col, i0 + lr, ld, ok);
-            fl_chain<KMAX, 1, SR>(x, p, sC, lr);
-            fl_store<1, NT>(x, col, i0 + lr, ld, ok);
-        }
-    }
-    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
-}
 
 // ------------------------------------------------------------------------
 // k_flushm: the flush on the matrix cores. A block of np pending pivots is
@@ -1934,99 +1773,6 @@ __global__ __launch_bounds__(kBlock, LB > 0 ? LB : 1) void k_flushm(double *__re
             for (int pp = 0; pp < NPAIR; pp++)
 #pragma unroll
                 for (int r = 0; r < 4; r++) t[pp][r] = tn[pp][r];
-        }
-    }
-    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
-}
-
-// k_flushs: the matrix-core flush with ONE column per lane (16 columns per
-// wave, 8-byte accesses, one 16x16 MFMA tile per 16-row step). Half the B
-// fragments of k_flushm per lane, so 64-pivot blocks keep 4+ waves per SIMD.
-// DYN: dynamic dequeue of items; otherwise a static grid stride.
-template <int KMAX, bool NT, int SR, bool DYN>
-__global__ __launch_bounds__(kBlock) void k_flushs(double *__restrict__ T, Geo g, DevState *__restrict__ st,
-                                                   const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
-                                                   int64_t cs, int64_t ntiles, int64_t nitems, int skip) {
-    constexpr int G = KMAX / 4;
-    __shared__ __attribute__((aligned(16))) double sC[KMAX * SR];
-    const int np = (int)st->npend;
-    if (np <= 0) return;
-    const int64_t ld = g.ld;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int lc = lane & 15, lk = lane >> 4;
-    unsigned long long touched = 0;
-    __shared__ int64_t next_item;
-    for (int64_t item = DYN ? -1 : blockIdx.x;; item += DYN ? 0 : gridDim.x) {
-        if (DYN) {
-            __syncthreads();
-            if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
-            __syncthreads();
-            item = next_item;
-        } else {
-            __syncthreads();   // sC of the previous item is no longer read
-        }
-        if (item >= nitems) break;
-        const int64_t tile = item % ntiles, strip = item / ntiles;
-        const int64_t i0 = strip * SR;
-        const int64_t i1 = i0 + SR < g.nloc ? i0 + SR : g.nloc;
-        const int64_t col = tile * 64 + wave * 16 + lc;
-        const bool in = col < g.ncols;
-        double b[G];
-        bool live = false;
-#pragma unroll
-        for (int gq = 0; gq < G; gq++) {
-            const int q = 4 * gq + lk;
-            b[gq] = (in && q < np) ? Pbuf[(int64_t)q * ld + col] : 0.0;
-            live = live || b[gq] != 0.0;
-        }
-        live = (__shfl_xor((int)live, 16, 64) | (int)live) != 0;
-        live = (__shfl_xor((int)live, 32, 64) | (int)live) != 0;
-        const bool ok = in && (!skip || live);
-        const int cnt = __syncthreads_count(ok);    // 4 lanes per column
-        if (cnt == 0) continue;
-        if (threadIdx.x == 0) touched += (unsigned long long)(cnt / 4) * (unsigned long long)(i1 - i0);
-        for (int e = threadIdx.x; e < KMAX * SR / 2; e += kBlock) {
-            const int q = e / (SR / 2), rr = 2 * (e % (SR / 2));
-            d2 v = d2{0.0, 0.0};
-            if (q < np && i0 + rr < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + i0 + rr);   // i0 + rr + 1 < cs
-            *(d2 *)(sC + q * SR + rr) = v;
-        }
-        __syncthreads();
-        double *cp = T + col;
-        d4 t;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int64_t row = i0 + lk + 4 * r;
-            const double *a = cp + row * ld;
-            t[r] = (ok && row < i1) ? (NT ? __builtin_nontemporal_load(a) : *a) : 0.0;
-        }
-        for (int64_t i = i0;;) {
-            const bool more = i + 16 < i1;
-            d4 tn;
-            if (more) {
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int64_t row = i + 16 + lk + 4 * r;
-                    const double *a = cp + row * ld;
-                    tn[r] = (ok && row < i1) ? (NT ? __builtin_nontemporal_load(a) : *a) : 0.0;
-                }
-            }
-            const int lr = (int)(i - i0) + lc;
-#pragma unroll
-            for (int gq = 0; gq < G; gq++)
-                t = __builtin_amdgcn_mfma_f64_16x16x4f64(-sC[(4 * gq + lk) * SR + lr], b[gq], t, 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int64_t row = i + lk + 4 * r;
-                if (ok && row < i1) {
-                    double *d = cp + row * ld;
-                    if (NT) __builtin_nontemporal_store(t[r], d);
-                    else *d = t[r];
-                }
-            }
-            if (!more) break;
-            i += 16;
-            t = tn;
         }
     }
     if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
@@ -2464,50 +2210,6 @@ int launch_iota(const Launch &L, int32_t *a, int64_t n) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-struct FlushCfg {
-    int mfma;         // 1: k_flushm (matrix cores), 0: k_flush (VALU fma, C through LDS)
-    int ru;           // VALU: rows per batch; MFMA: column pairs per wave (NPAIR)
-    bool nt, pipe;
-    int strip;        // rows per work item (VALU: compile-time LDS tile of C)
-    int per_cu;       // persistent blocks per CU
-};
-
-// Flush variant table (LPG_FLUSH_VARIANT); every variant is bit-identical.
-static const FlushCfg kFlushCfgs[] = {
-    {0, 8, true, true, 64, 4},      // 0
-    {0, 8, true, false, 64, 4},     // 1
-    {0, 4, true, true, 64, 4},      // 2
-    {0, 8, false, true, 64, 4},     // 3
-    {0, 8, true, true, 32, 4},      // 4
-    {0, 8, true, true, 128, 2},     // 5
-    {0, 16, true, false, 64, 4},    // 6
-    {0, 4, true, false, 32, 8},     // 7
-    {1, 1, true, true, 128, 4},     // 8  MFMA, 32 columns per wave
-    {1, 2, true, true, 128, 4},     // 9  MFMA, 64 columns per wave
-    {1, 1, false, true, 64, 8},     // 10
-    {1, 1, true, true, 64, 8},      // 11
-    {1, 1, true, true, 32, 8},      // 12
-    {1, 1, true, true, 32, 4},      // 13
-    {2, 1, true, true, 64, 4},      // 14 MFMA, one column per lane, dynamic dequeue
-    {2, 0, true, true, 64, 4},      // 15 same, static grid stride
-    {2, 1, true, true, 128, 2},     // 16 128-row strips
-    {2, 1, false, true, 64, 4},     // 17 temporal loads / stores
-    {2, 0, true, true, 64, 8},      // 18 static, 8 blocks per CU
-    {1, 1, true, true, 128, 104},   // 19 = 8 with __launch_bounds__(256, 3) and grouped A fragments
-    {1, 1, true, true, 64, 104},    // 20 same, 64-row strips
-    {3, 2, true, true, 512, 0},     // 21 k_flushw: 512-row items, 2-deep C ring (blocks/CU: 2 at 64 slots, else 3)
-    {3, 3, true, true, 512, 0},     // 22 same, 3-deep ring
-    {3, 2, true, true, 256, 0},     // 23 256-row items
-    {3, 2, true, true, 1024, 0},    // 24 1024-row items
-    {3, 2, true, true, 512, 8},     // 25 k_flushw, 8-wave blocks (256-column tiles; 4 waves below 64 slots)
-    {3, 2, true, true, 1024, 8},    // 26 same, 1024-row items
-    {3, 3, true, true, 512, 8},     // 27 same, 3-deep ring
-    {3, 2, true, true, 256, 8},     // 28 same, 256-row items
-};
-constexpr int kNumFlushCfgs = sizeof(kFlushCfgs) / sizeof(kFlushCfgs[0]);
-constexpr int kDefaultFlushCfg = 8;       // blocks of <= 32 pivots: k_flushm
-constexpr int kDefaultFlushCfg64 = 21;    // 64-pivot blocks: k_flushw
-
 int flush_kmax_supported(int k) {
     if (k <= 8) return 8;
     if (k <= 16) return 16;
@@ -2537,142 +2239,57 @@ int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, in
     return rc ? rc : launch_flush_tail(L, g, st, D, kmax);
 }
 
-int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant) {
+// which: -1 = default (k_flushm for blocks of <= 32 pivots, k_flushw for 64),
+// 0 = k_flushm, 1 = k_flushw (LPG_FLUSH_KERNEL=m|w, tests). Both bitwise.
+int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which) {
     kmax = flush_kmax_supported(kmax);
     if (!kmax) return -1;
-    if (variant < 0 || variant >= kNumFlushCfgs) variant = kmax == 64 ? kDefaultFlushCfg64 : kDefaultFlushCfg;
-    FlushCfg cfg = kFlushCfgs[variant];
+    if (which < 0) which = kmax == 64 ? 1 : 0;
+    if (kmax == 64) which = 1;                              // k_flushm's C tile caps it at 32 slots
     hipStream_t stream = (hipStream_t)L.stream;
-    if (cfg.mfma == 3) {                                     // k_flushw: ru = ring depth, strip = rows per item,
-        const int wpb = (cfg.per_cu == 8 && kmax == 64) ? 8 : 4;   // per_cu = waves per block
-        const int64_t ntiles = (g.ncols + 32 * wpb - 1) / (32 * wpb);
-        int64_t rows = cfg.strip;
-        while (rows > 64 && ntiles * ((g.nloc + rows - 1) / rows) < 2048 / (wpb / 4)) rows /= 2;   // small tableaus: fill the chip
+    if (which == 1) {
+        // k_flushw: 4-wave blocks, 128-column x 512-row items swept in 16-row
+        // bands with a 2-deep LDS ring of multipliers; small tableaus shrink
+        // the items until they fill the chip
+        const int64_t ntiles = (g.ncols + 127) / 128;
+        int64_t rows = 512;
+        while (rows > 64 && ntiles * ((g.nloc + rows - 1) / rows) < 2048) rows /= 2;
         const int64_t nitems = ntiles * ((g.nloc + rows - 1) / rows);
-        // VGPRs: 184 at 64 slots, <= 128 below (8-32: the 32 form); 8-wave blocks: one per CU
-        const int lb = wpb == 8 ? 1 : kmax == 64 ? 2 : 3;
+        const int lb = kmax == 64 ? 2 : 3;                  // VGPRs: 184 at 64 slots, <= 128 below
         const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * lb);
         if (nblocks < 1) return 0;
-#define LPG_FW(K, NB, LBV, W)                                                                                     \
-    hipLaunchKernelGGL((k_flushw<K, NB, LBV, W>), dim3((unsigned)nblocks), dim3(64 * W), 0, stream, g.T, g, st, \
-                       D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip)
-#define LPG_FW_K(NB)                                  \
-    if (wpb == 8) {                                   \
-        LPG_FW(64, NB, 1, 8);                         \
-    } else {                                          \
-        switch (kmax) {                               \
-            case 64: LPG_FW(64, NB, 2, 4); break;     \
-            default: LPG_FW(32, NB, 3, 4); break;     \
-        }                                             \
-    }
-        if (cfg.ru == 3) { LPG_FW_K(3) }
-        else { LPG_FW_K(2) }
-#undef LPG_FW_K
-#undef LPG_FW
-    } else if (cfg.mfma == 2) {                                     // k_flushs: ru = DYN
-        const int64_t ntiles = (g.ncols + 63) / 64;
-        int strip = cfg.strip;
+        if (kmax == 64)
+            hipLaunchKernelGGL((k_flushw<64, 2, 2, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
+                               D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
+        else
+            hipLaunchKernelGGL((k_flushw<32, 2, 3, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
+                               D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
+    } else {
+        // k_flushm: 32-column wave tiles, 128-row strips (C tile <= 32 KB of LDS),
+        // shorter strips for small tableaus; 4 blocks per CU
+        const int64_t ntiles = (g.ncols + 127) / 128;
+        int strip = 128;
         while (strip > 32 && ntiles * ((g.nloc + strip - 1) / strip) < 4096) strip /= 2;
-        while (strip > 32 && kmax * strip * 8 > 65536) strip /= 2;   // LDS tile of C <= 64 KB
+        while (strip > 32 && kmax * strip * 8 > 32768) strip /= 2;
         const int64_t nitems = ntiles * ((g.nloc + strip - 1) / strip);
-        const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * cfg.per_cu);
+        const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * 4);
         if (nblocks < 1) return 0;
-#define LPG_FS(K, N, S, DY)                                                                                          \
-    hipLaunchKernelGGL((k_flushs<K, N, S, DY>), dim3((unsigned)nblocks), dim3(kBlock), 0, stream, g.T, g, st, D.Pbuf, \
-                       D.Cbuf, D.cs, ntiles, nitems, skip)
-#define LPG_FS_S(K, N, DY)                       \
-    switch (strip) {                             \
-        case 32: LPG_FS(K, N, 32, DY); break;    \
-        case 64: LPG_FS(K, N, 64, DY); break;    \
-        default: LPG_FS(K, N, 128, DY); break;   \
+#define LPG_FM(K, S)                                                                                                 \
+    hipLaunchKernelGGL((k_flushm<K, 1, true, S, 0>), dim3((unsigned)nblocks), dim3(kBlock), 0, stream, g.T, g, st,    \
+                       D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, skip)
+#define LPG_FM_S(K)                                                              \
+    switch (strip) {                                                             \
+        case 32: LPG_FM(K, 32); break;                                           \
+        case 64: LPG_FM(K, (K * 64 * 8 <= 32768 ? 64 : 32)); break;              \
+        default: LPG_FM(K, (K * 128 * 8 <= 32768 ? 128 : 64)); break;            \
     }
-#define LPG_FS_K(N, DY)                          \
-    switch (kmax) {                              \
-        case 8: LPG_FS_S(8, N, DY); break;       \
-        case 16: LPG_FS_S(16, N, DY); break;     \
-        case 32: LPG_FS_S(32, N, DY); break;     \
-        default: LPG_FS_S(64, N, DY); break;     \
-    }
-        if (cfg.nt) { if (cfg.ru) LPG_FS_K(true, true) else LPG_FS_K(true, false) }
-        else { if (cfg.ru) LPG_FS_K(false, true) else LPG_FS_K(false, false) }
-#undef LPG_FS_K
-#undef LPG_FS_S
-#undef LPG_FS
-    } else if (cfg.mfma) {
-        const int64_t bcols = 4 * 32 * cfg.ru;
-        const int64_t ntiles = (g.ncols + bcols - 1) / bcols;
-        int strip = cfg.strip;
-        while (strip > 32 && ntiles * ((g.nloc + strip - 1) / strip) < 4096) strip /= 2;
-        while (strip > 32 && kmax * strip * 8 > 32768) strip /= 2;   // LDS tile of C <= 32 KB
-        const int64_t nitems = ntiles * ((g.nloc + strip - 1) / strip);
-        const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * (cfg.per_cu % 100));
-        if (nblocks < 1) return 0;
-#define LPG_FM(K, NP, N, S)                                                                                          \
-    do {                                                                                                             \
-        if (cfg.per_cu >= 100)                                                                                       \
-            hipLaunchKernelGGL((k_flushm<K, NP, N, S, (NP == 1 ? 3 : 0)>), dim3((unsigned)nblocks), dim3(kBlock), 0,   \
-                               stream, g.T, g, st, D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, skip);                       \
-        else                                                                                                         \
-            hipLaunchKernelGGL((k_flushm<K, NP, N, S, 0>), dim3((unsigned)nblocks), dim3(kBlock), 0, stream, g.T, g,  \
-                               st, D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, skip);                                       \
-    } while (0)
-// strips are capped so that the C tile stays <= 32 KB (the launcher guarantees it; the
-// expressions keep larger tiles from being instantiated at all)
-#define LPG_FM_S(K, NP, N)                                                              \
-    switch (strip) {                                                                    \
-        case 32: LPG_FM(K, NP, N, 32); break;                                           \
-        case 64: LPG_FM(K, NP, N, (K * 64 * 8 <= 32768 ? 64 : 32)); break;              \
-        default: LPG_FM(K, NP, N, (K * 128 * 8 <= 32768 ? 128 : 64)); break;            \
-    }
-#define LPG_FM_K(NP, N)                         \
-    switch (kmax) {                             \
-        case 8: LPG_FM_S(8, NP, N); break;      \
-        case 16: LPG_FM_S(16, NP, N); break;    \
-        case 32: LPG_FM_S(32, NP, N); break;    \
-        default: LPG_FM_S(64, NP, N); break;    \
-    }
-        if (cfg.ru == 2) { if (cfg.nt) LPG_FM_K(2, true) else LPG_FM_K(2, false) }
-        else { if (cfg.nt) LPG_FM_K(1, true) else LPG_FM_K(1, false) }
-#undef LPG_FM_K
+        switch (kmax) {
+            case 8: LPG_FM_S(8); break;
+            case 16: LPG_FM_S(16); break;
+            default: LPG_FM_S(32); break;
+        }
 #undef LPG_FM_S
 #undef LPG_FM
-    } else {
-        const int64_t ntiles = (g.ncols + kBlock - 1) / kBlock;   // columns of 256
-        // small tableaus: 32-row strips so that the items fill the chip
-        if (ntiles * ((g.nloc + cfg.strip - 1) / cfg.strip) < 4096) cfg.strip = 32;
-        // the LDS tile is KMAX x strip doubles: keep it within 64 KB
-        while (cfg.strip > 32 && kmax * cfg.strip * 8 > 65536) cfg.strip /= 2;
-        const int64_t nitems = ntiles * ((g.nloc + cfg.strip - 1) / cfg.strip);
-        const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * cfg.per_cu);
-        if (nblocks < 1) return 0;
-        dim3 grid((unsigned)nblocks), blk(kBlock);
-#define LPG_FL(K, R, N, PI, S)                                                                                   \
-    hipLaunchKernelGGL((k_flush<K, R, N, PI, S>), grid, blk, 0, stream, g.T, g, st, D.Pbuf, D.Cbuf, D.cs, ntiles, \
-                       nitems, skip)
-#define LPG_FL_S(K, R, N, PI)                                   \
-    switch (cfg.strip) {                                        \
-        case 32: LPG_FL(K, R, N, PI, 32); break;                \
-        case 64: LPG_FL(K, R, N, PI, 64); break;                \
-        default: LPG_FL(K, R, N, PI, 128); break;               \
-    }
-#define LPG_FL_K(R, N, PI)                       \
-    switch (kmax) {                              \
-        case 8: LPG_FL_S(8, R, N, PI); break;    \
-        case 16: LPG_FL_S(16, R, N, PI); break;  \
-        case 32: LPG_FL_S(32, R, N, PI); break;  \
-        default: LPG_FL_S(64, R, N, PI); break;  \
-    }
-        switch (variant) {
-            case 1: LPG_FL_K(8, true, false); break;
-            case 2: LPG_FL_K(4, true, true); break;
-            case 3: LPG_FL_K(8, false, true); break;
-            case 6: LPG_FL_K(16, true, false); break;
-            case 7: LPG_FL_K(4, true, false); break;
-            default: LPG_FL_K(8, true, true); break;
-        }
-#undef LPG_FL_K
-#undef LPG_FL_S
-#undef LPG_FL
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -46,6 +46,12 @@ double lpo_uniform(uint64_t key, uint64_t idx) {
     return (double)(splitmix64(key ^ (idx * 0x9E3779B97F4A7C15ull)) >> 11) * 0x1.0p-53;
 }
 
+int lpo_set_threads(lpo_ctx *c, int nthreads) {
+    if (!c || nthreads < 1) return -1;
+    c->nthreads = nthreads;
+    return 0;
+}
+
 lpo_ctx *lpo_create(int64_t m, int64_t ncols, int nthreads) { return lpo_create2(m, ncols, nthreads, 1); }
 
 lpo_ctx *lpo_create2(int64_t m, int64_t ncols, int nthreads, int nobj) {

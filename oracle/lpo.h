@@ -62,6 +62,8 @@ lpo_ctx *lpo_create(int64_t m, int64_t ncols, int nthreads);
 /* nobj = 2: Big-M layout (row m = M part, row m+1 = real part). */
 lpo_ctx *lpo_create2(int64_t m, int64_t ncols, int nthreads, int nobj);
 void     lpo_destroy(lpo_ctx *ctx);
+/* OpenMP threads of the row loops from now on (bench.py's 1-core CPU baseline). */
+int      lpo_set_threads(lpo_ctx *ctx, int nthreads);
 int      lpo_load_rows(lpo_ctx *ctx, int64_t row0, int64_t nrows, const double *rows, int64_t ld);
 int      lpo_set_basis(lpo_ctx *ctx, const int64_t *basis);
 /* Objective row from costs c[0..N-1] (max c.x) and the current basis:

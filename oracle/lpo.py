@@ -55,6 +55,7 @@ def load():
             "lpo_solve_big_m": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _dp, ctypes.c_int64, ctypes.c_int,
                                                ctypes.POINTER(_Result)]),
             "lpo_destroy": (None, [ctypes.c_void_p]),
+            "lpo_set_threads": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
             "lpo_load_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, _dp, ctypes.c_int64]),
             "lpo_set_basis": (ctypes.c_int, [ctypes.c_void_p, _ip]),
             "lpo_set_objective": (ctypes.c_int, [ctypes.c_void_p, _dp]),
@@ -92,6 +93,9 @@ class Oracle:
         self.ctx = self.lib.lpo_create2(m, ncols, nthreads, nobj)
         if not self.ctx:
             raise RuntimeError("lpo_create failed")
+
+    def set_threads(self, n: int):
+        self._ok(self.lib.lpo_set_threads(self.ctx, n), "set_threads")
 
     def close(self):
         if self.ctx:

@@ -104,10 +104,10 @@ def test_enqueue_past_optimal_partial_block(lpg, monkeypatch):
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("k", [32, 64])
-@pytest.mark.parametrize("variant", list(range(29)))
-def test_flush_variants_identical(lpg, monkeypatch, variant, k):
-    monkeypatch.setenv("LPG_FLUSH_VARIANT", str(variant))
+@pytest.mark.parametrize("kernel,k", [("m", 8), ("m", 16), ("m", 32), ("w", 8), ("w", 32), ("w", 64)])
+def test_flush_kernels_identical(lpg, monkeypatch, kernel, k):
+    """k_flushm and k_flushw at their block sizes (LPG_FLUSH_KERNEL forces one)."""
+    monkeypatch.setenv("LPG_FLUSH_KERNEL", kernel)
     m, n = 300, 700
     e = _engine(lpg, monkeypatch, k, m, n + m + 1)
     o = Oracle(m, n + m + 1)
@@ -151,14 +151,13 @@ def test_bad_block_size(lpg, monkeypatch):
         lpg.Engine(8, 20)
 
 
-@pytest.mark.parametrize("variant", [7, 8, 9, 14, 15, 19, 21, 22, 23, 25, 26])
-@pytest.mark.parametrize("k", [3, 8, 32, 64])
+@pytest.mark.parametrize("kernel,k", [("m", 3), ("m", 8), ("m", 32), ("w", 3), ("w", 32), ("w", 64)])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1)])
-def test_flush_kernels_block_sizes(lpg, monkeypatch, variant, k, m, n, seed, kind, rule):
-    """VALU (7), matrix-core (8, 9, 14, 15, 19) and tall-item banded (21-23; 25-26 8-wave blocks)
-    flushes at every compiled block bound, to optimality, against the oracle
-    (odd shapes: ragged column tiles, strips and bands)."""
-    monkeypatch.setenv("LPG_FLUSH_VARIANT", str(variant))
+def test_flush_kernels_block_sizes(lpg, monkeypatch, kernel, k, m, n, seed, kind, rule):
+    """k_flushm (strip-staged C) and k_flushw (tall banded items) at every
+    compiled block bound, to optimality, against the oracle (odd shapes: ragged
+    column tiles, strips and bands)."""
+    monkeypatch.setenv("LPG_FLUSH_KERNEL", kernel)
     e = _engine(lpg, monkeypatch, k, m, n + m + 1)
     o = Oracle(m, n + m + 1)
     e.generate(n, seed, kind)

@@ -211,7 +211,7 @@ def test_set_objective_general_basis(lpg):
     assert res.status == ores.status and res.objective == ores.objective
 
 
-@pytest.mark.parametrize("variant", list(range(25)))
+@pytest.mark.parametrize("variant", [0, 1])
 def test_update_variants_identical(lpg, variant, monkeypatch):
     monkeypatch.setenv("LPG_DEFER", "0")            # the per-pivot update kernel runs in eager mode
     monkeypatch.setenv("LPG_UPDATE_VARIANT", str(variant))

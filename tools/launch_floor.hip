@@ -23,10 +23,16 @@ __global__ void k_chain(const int *idx, int *out, int hops) {
 // 2: poll with a system-scope load; each with a release fence before arriving
 // and an acquire fence after leaving. A data word written by every block
 // before the barrier is checked by block 0 after it (stale reads counted).
+// The words are double-buffered by round parity: a block that has left
+// round r's barrier writes round r+1's word into the other half, so block
+// 0's check of round r can only see round r's value or an older (stale) one.
+// (Round 1 used one buffer, so faster blocks' round r+1 writes were counted
+// as "stale" -- they were too new; profiles/r01_launch_floor.log.)
 template <int MODE>
 __global__ void k_barrier(unsigned long long *bar, int rounds, int nb, unsigned long long *data, unsigned long long *bad) {
     for (int r = 0; r < rounds; r++) {
-        if (threadIdx.x == 0) data[blockIdx.x] = (unsigned long long)r * 1000003ull + blockIdx.x;
+        unsigned long long *dr = data + (r & 1) * nb;
+        if (threadIdx.x == 0) dr[blockIdx.x] = (unsigned long long)r * 1000003ull + blockIdx.x;
         __syncthreads();
         if (threadIdx.x == 0) {
             __threadfence();
@@ -46,7 +52,7 @@ __global__ void k_barrier(unsigned long long *bar, int rounds, int nb, unsigned 
         }
         __syncthreads();
         if (blockIdx.x == 0 && threadIdx.x < nb) {
-            unsigned long long v = __hip_atomic_load(&data[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned long long v = __hip_atomic_load(&dr[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (v != (unsigned long long)r * 1000003ull + threadIdx.x) atomicAdd(bad, 1ull);
         }
         __syncthreads();
@@ -117,7 +123,7 @@ int main() {
         printf("dependent loads x%d:        graph %6.2f us\n", hops,
                graph_time(s, N, [&] { hipLaunchKernelGGL(k_chain, dim3(97), dim3(256), 0, s, idx, out, hops); }));
     unsigned long long *data, *bad;
-    CHK(hipMalloc(&data, 1024 * 8)); CHK(hipMalloc(&bad, 8));
+    CHK(hipMalloc(&data, 2 * 1024 * 8)); CHK(hipMalloc(&bad, 8));
     for (int mode = 1; mode < 3; mode++)
     for (int nb = 4; nb <= 256; nb *= 4) {
         hipEvent_t e0, e1;
