@@ -1,18 +1,28 @@
 // flush_lab.hip — standalone bench of deferred-flush kernel designs at the
 // config-3 shape (16384 constraint rows x 49153 columns, ld 49216, fp64), on
 // random T / Pbuf / Cbuf with the slack block's P entries zero (skipped, as in
-// the first blocks of a solve). Every design is checked bitwise against the
-// engine's default flush (launch_flush) before it is timed. Tools only: the
-// product never links this file.
+// the first blocks of a solve). Blocks of 128 pending pivots: the reference is
+// the engine's k_flushw<64> run twice (slots 0-63, then 64-127), which is the
+// same per-element fma chain; every design is checked bitwise against it
+// before it is timed. Tools only: the product never links this file.
+//
+// Round-2 result (profiles/r02_flush_lab_k128.log): no 128-slot design beats
+// two 64-slot passes by enough to pay for 128-slot pivot chains. 2 x
+// k_flushw<64> 3.31-3.36 ms; k_flushw<128> (1 wave/SIMD, 256 VGPR + AGPRs)
+// 3.00 ms; k_flushx (A through LDS-DMA, 4 chains) 3.54 ms; k_flushy (roles
+// swapped, P tile in LDS, no block barrier) 3.39 ms. k_flushy's parts: memory
+// alone (no MFMA) 1.83 ms = 4.7 TB/s, matrix cores alone (no tableau traffic)
+// 2.93 ms = 47 TFLOP/s of the 75 the f64 MFMA pipe reaches: at 128 slots the
+// operands no longer fit beside a prefetch set, the compiler serialises each
+// LDS read of B behind the MFMAs that consume the previous one, and 1 wave
+// per SIMD cannot hide it.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o tools/flush_lab tools/flush_lab.hip
-//   tools/flush_lab [K] [rows]
+//   tools/flush_lab [rows]            (LAB_ONLY=substring picks designs)
 #include "../linearprogramming_amd/csrc/lpg_kernels.hip"
 
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
-
-#include <vector>
 
 #define CHK(x)                                                                      \
     do {                                                                            \
@@ -25,114 +35,27 @@
 
 namespace lpg {
 
-// k_flushr: 16 columns per wave (8-byte accesses), NSUB independent 16-row
-// MFMA chains per iteration sharing the B fragments, multipliers staged
-// negated in a padded LDS tile, the next iteration's rows loaded ahead.
-template <int KMAX, int SR, int NSUB>
-__global__ __launch_bounds__(kBlock) void k_flushr(double *__restrict__ T, Geo g, DevState *__restrict__ st,
-                                                   const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
-                                                   int64_t cs, int64_t ntiles, int64_t nitems, int skip) {
+// k_flushx: 128-slot blocks. Wave tile 32 columns (16-byte accesses, even /
+// odd-column MFMA chains as k_flushw) x SB bands of 16 rows per step, so a
+// wave runs 2*SB independent MFMA chains; B = -P in VGPRs for the item; the
+// multipliers (raw C, A fragments) come into a 2-deep LDS ring straight from
+// global memory (global_load_lds, 16 B per lane, lane-linear [band][q][16
+// rows] image), slots past np read from a zero row. fma(c, -p, x) ==
+// fma(-c, p, x) bit for bit, and for q >= np A = +0, B = -0: x + (+0)(-0) ==
+// x for every x, signed zeros included.
+template <int KMAX, int SB, int LB>
+__global__ __launch_bounds__(256, LB) void k_flushx(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                    const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
+                                                    int64_t cs, int64_t ntiles, int64_t nitems, int64_t rows, int skip,
+                                                    const double *__restrict__ zbuf) {
     constexpr int G = KMAX / 4;
-    constexpr int SRP = SR + 16;
-    constexpr int RI = 16 * NSUB;
-    static_assert(SR % RI == 0, "strip must hold whole iterations");
-    __shared__ __attribute__((aligned(16))) double sC[KMAX * SRP];
+    constexpr int STEP = 16 * SB;                 // rows per step
+    constexpr int SD = KMAX * STEP;               // doubles of A per step
+    constexpr int GL = SD / 2 / 256;              // 16-byte LDS-DMA pieces per thread per step
+    static_assert(GL >= 1 && (SD / 2) % 256 == 0, "staging");
+    __shared__ __attribute__((aligned(16))) double sA[2][SD];
     __shared__ int64_t next_item;
-    const int np = (int)st->npend;
-    if (np <= 0) return;
-    const int64_t ld = g.ld;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int lc = lane & 15, lk = lane >> 4;
-    unsigned long long touched = 0;
-    for (;;) {
-        __syncthreads();
-        if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
-        __syncthreads();
-        const int64_t item = next_item;
-        if (item >= nitems) break;
-        const int64_t tile = item % ntiles, strip = item / ntiles;
-        const int64_t i0 = strip * SR;
-        const int64_t i1 = i0 + SR < g.nloc ? i0 + SR : g.nloc;
-        const int64_t col = tile * 64 + wave * 16 + lc;
-        const bool in = col < g.ncols;
-        double b[G];
-        bool live = false;
-#pragma unroll
-        for (int gq = 0; gq < G; gq++) {
-            const int q = 4 * gq + lk;
-            b[gq] = (in && q < np) ? Pbuf[(int64_t)q * ld + col] : 0.0;
-            live = live || b[gq] != 0.0;
-        }
-        live = (__shfl_xor((int)live, 16, 64) | (int)live) != 0;
-        live = (__shfl_xor((int)live, 32, 64) | (int)live) != 0;
-        const bool ok = in && (!skip || live);
-        const int cnt = __syncthreads_count(ok);
-        if (cnt == 0) continue;
-        if (threadIdx.x == 0) touched += (unsigned long long)(cnt / 4) * (unsigned long long)(i1 - i0);
-        for (int e = threadIdx.x; e < KMAX * SR / 2; e += kBlock) {
-            const int q = e / (SR / 2), rr = 2 * (e % (SR / 2));
-            d2 v = d2{0.0, 0.0};
-            if (q < np && i0 + rr < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + i0 + rr);
-            *(d2 *)(sC + q * SRP + rr) = -v;
-        }
-        __syncthreads();
-        double *cp = T + col;
-        double t[NSUB][4];
-        auto load = [&](double (&x)[NSUB][4], int64_t i) {
-#pragma unroll
-            for (int s = 0; s < NSUB; s++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int64_t row = i + 16 * s + lk + 4 * r;
-                    x[s][r] = (ok && row < i1) ? __builtin_nontemporal_load(cp + row * ld) : 0.0;
-                }
-        };
-        int64_t i = i0;
-        load(t, i);
-        for (;;) {
-            const bool more = i + RI < i1;
-            double tn[NSUB][4];
-            if (more) load(tn, i + RI);
-            d4 acc[NSUB];
-#pragma unroll
-            for (int s = 0; s < NSUB; s++) acc[s] = d4{t[s][0], t[s][1], t[s][2], t[s][3]};
-            const double *sa = sC + lk * SRP + (int)(i - i0) + lc;
-#pragma unroll
-            for (int gq = 0; gq < G; gq++) {
-#pragma unroll
-                for (int s = 0; s < NSUB; s++)
-                    acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[4 * gq * SRP + 16 * s], b[gq], acc[s], 0, 0, 0);
-            }
-#pragma unroll
-            for (int s = 0; s < NSUB; s++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int64_t row = i + 16 * s + lk + 4 * r;
-                    if (ok && row < i1) __builtin_nontemporal_store(acc[s][r], cp + row * ld);
-                }
-            if (!more) break;
-            i += RI;
-#pragma unroll
-            for (int s = 0; s < NSUB; s++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) t[s][r] = tn[s][r];
-        }
-    }
-    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
-}
-
-template <int KMAX, int NB, int LB>
-__global__ __launch_bounds__(kBlock, LB) void k_flushw2(double *__restrict__ T, Geo g, DevState *__restrict__ st,
-                                                       const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
-                                                       int64_t cs, int64_t ntiles, int64_t nitems, int64_t rows,
-                                                       int skip) {
-    constexpr int G = KMAX / 4;
-    constexpr int BAND = KMAX * 16;                 // doubles per band
-    constexpr int PER = BAND / 2 / kBlock;          // 16-byte multiplier pieces per thread per band
-    static_assert(PER >= 1 && BAND / 2 % kBlock == 0, "band staging");
-    __shared__ __attribute__((aligned(16))) double sC[NB][BAND];
-    __shared__ int64_t next_item;
-    __shared__ int wsum[kBlock / 64];
+    __shared__ int wsum[4];
     const int np = (int)st->npend;
     if (np <= 0) return;
     const int64_t ld = g.ld;
@@ -148,8 +71,8 @@ __global__ __launch_bounds__(kBlock, LB) void k_flushw2(double *__restrict__ T, 
         const int64_t tile = item % ntiles, strip = item / ntiles;
         const int64_t i0 = strip * rows;
         const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
-        const int64_t cl = tile * 128 + wave * 32 + 2 * lc;   // this lane's column pair
-        const bool in = cl < g.ncols;                         // cl even, ld even: cl + 1 < ld
+        const int64_t cl = tile * 128 + wave * 32 + 2 * lc;
+        const bool in = cl < g.ncols;
         double be[G], bo[G];
         bool live = false;
 #pragma unroll
@@ -157,96 +80,234 @@ __global__ __launch_bounds__(kBlock, LB) void k_flushw2(double *__restrict__ T, 
             const int q = 4 * gq + lk;
             d2 v = d2{0.0, 0.0};
             if (in && q < np) v = *(const d2 *)(Pbuf + (int64_t)q * ld + cl);
-            be[gq] = v.x;
-            bo[gq] = v.y;
             live = live || v.x != 0.0 || v.y != 0.0;
+            be[gq] = -v.x;
+            bo[gq] = -v.y;
         }
-        // a column pair is live if any of its P entries over all slots is
-        // non-zero: OR over the 4 lanes holding its k-slices
         live = (__shfl_xor((int)live, 16, 64) | (int)live) != 0;
         live = (__shfl_xor((int)live, 32, 64) | (int)live) != 0;
         const bool ok = in && (!skip || live);
-        // per-chain liveness: the even (odd) chain runs if any even (odd) column of the wave is live
-        bool le = false, lo = false;
-#pragma unroll
-        for (int gq = 0; gq < G; gq++) {
-            le = le || be[gq] != 0.0;
-            lo = lo || bo[gq] != 0.0;
-        }
-        const bool run_e = !skip || __ballot(in && le) != 0, run_o = !skip || __ballot(in && lo && cl + 1 < g.ncols) != 0;
-        int mine = (lk == 0 && ok) ? (cl + 1 < g.ncols ? 2 : 1) : 0;   // live doubles per row, pairs counted once
+        int mine = (lk == 0 && ok) ? (cl + 1 < g.ncols ? 2 : 1) : 0;
         for (int mask = 32; mask > 0; mask >>= 1) mine += __shfl_xor(mine, mask, 64);
-        const bool wlive = mine > 0;                                   // wave-uniform
+        const bool wlive = mine > 0;
         if (lane == 0) wsum[wave] = mine;
-        if (__syncthreads_count(wlive && lane == 0) == 0) continue;    // the whole tile is skipped
-        if (threadIdx.x == 0)
-            touched += (unsigned long long)(wsum[0] + wsum[1] + wsum[2] + wsum[3]) * (unsigned long long)(i1 - i0);
-        const int nb = (int)((i1 - i0 + 15) / 16);
-        // multiplier piece e of band s: slot q = e / 8, band rows 2 (e % 8) .. +1
-        // (zeros past np and past i1: A = -0 there, x + -0 == x)
-        auto cload = [&](d2 (&cr)[PER], int s) {
+        if (__syncthreads_count(wlive && lane == 0) == 0) continue;
+        if (threadIdx.x == 0) touched += (unsigned long long)(wsum[0] + wsum[1] + wsum[2] + wsum[3]) * (i1 - i0);
+        const int nst = (int)((i1 - i0 + STEP - 1) / STEP);
+        // A image of step s: element e (16 B) = doubles 2e, 2e+1 of [b][q][16]
+        auto aload = [&](int s, int slot) {
 #pragma unroll
-            for (int u = 0; u < PER; u++) {
-                const int e = threadIdx.x + u * kBlock;
-                const int q = e >> 3, rr = 2 * (e & 7);
-                const int64_t row = i0 + 16 * s + rr;
-                d2 v = d2{0.0, 0.0};
-                if (s < nb && q < np && row < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + row);   // row + 1 < cs
-                cr[u] = -v;
+            for (int u = 0; u < GL; u++) {
+                const int e = u * 256 + threadIdx.x;
+                const int d = 2 * e;
+                const int b = d / (KMAX * 16), q = (d / 16) % KMAX, rr = d % 16;
+                const int64_t row = i0 + (int64_t)s * STEP + 16 * b + rr;
+                const double *src = (q < np && s < nst) ? Cbuf + (int64_t)q * cs + row : zbuf;
+                __builtin_amdgcn_global_load_lds((const void *)src, (void *)&sA[slot][2 * (u * 256 + wave * 64)], 16, 0, 0);
             }
         };
-        auto cstore = [&](const d2 (&cr)[PER], int s) {
+        auto tload = [&](d2 (&x)[SB][4], int s) {
 #pragma unroll
-            for (int u = 0; u < PER; u++) *(d2 *)(&sC[s % NB][2 * (threadIdx.x + u * kBlock)]) = cr[u];
-        };
-        for (int s = 0; s < NB - 1; s++) {   // prologue: bands 0 .. NB-2 into the ring
-            d2 cr[PER];
-            cload(cr, s);
-            cstore(cr, s);
-        }
-        d2 cn[PER];
-        cload(cn, NB - 1);
-        auto tload = [&](d2 (&x)[4], int s) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int64_t row = i0 + 16 * s + lk + 4 * r;
-                x[r] = (ok && row < i1) ? __builtin_nontemporal_load((const d2 *)(T + row * ld + cl)) : d2{0.0, 0.0};
-            }
-        };
-        d2 t[4];
-        tload(t, 0);
-        for (int s = 0; s < nb; s++) {
-            d2 tn[4];
-            if (s + 1 < nb) tload(tn, s + 1);
-            __syncthreads();                  // band s is staged; ring slot (s - 1) % NB is free
-            cstore(cn, s + NB - 1);
-            cload(cn, s + NB);
-            if (wlive) {
-                d4 ae = d4{t[0].x, t[1].x, t[2].x, t[3].x};
-                d4 ao = d4{t[0].y, t[1].y, t[2].y, t[3].y};
-                const double *sa = &sC[s % NB][lk * 16 + lc];
-                if (run_e && run_o) {
-#pragma unroll
-                    for (int gq = 0; gq < G; gq++) {
-                        const double a = sa[gq * 64];
-                        ae = __builtin_amdgcn_mfma_f64_16x16x4f64(a, be[gq], ae, 0, 0, 0);
-                        ao = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bo[gq], ao, 0, 0, 0);
-                    }
-                } else if (run_e) {
-#pragma unroll
-                    for (int gq = 0; gq < G; gq++) ae = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[gq * 64], be[gq], ae, 0, 0, 0);
-                } else {
-#pragma unroll
-                    for (int gq = 0; gq < G; gq++) ao = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[gq * 64], bo[gq], ao, 0, 0, 0);
-                }
+            for (int b = 0; b < SB; b++)
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
-                    const int64_t row = i0 + 16 * s + lk + 4 * r;
-                    if (ok && row < i1) __builtin_nontemporal_store(d2{ae[r], ao[r]}, (d2 *)(T + row * ld + cl));
+                    const int64_t row = i0 + (int64_t)s * STEP + 16 * b + lk + 4 * r;
+                    x[b][r] = (ok && row < i1) ? __builtin_nontemporal_load((const d2 *)(T + row * ld + cl))
+                                               : d2{0.0, 0.0};
                 }
+        };
+        d2 t[SB][4];
+        aload(0, 0);
+        tload(t, 0);
+        for (int s = 0; s < nst; s++) {
+            // A of step s (and the tableau of step s) have landed; the stores of step s - 1 may be in flight
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * SB) : "memory");
+            __builtin_amdgcn_s_barrier();
+            d2 tn[SB][4];
+            if (s + 1 < nst) {
+                aload(s + 1, (s + 1) & 1);
+                tload(tn, s + 1);
+            }
+            if (wlive) {
+                d4 ae[SB], ao[SB];
+#pragma unroll
+                for (int b = 0; b < SB; b++) {
+                    ae[b] = d4{t[b][0].x, t[b][1].x, t[b][2].x, t[b][3].x};
+                    ao[b] = d4{t[b][0].y, t[b][1].y, t[b][2].y, t[b][3].y};
+                }
+                const double *sa = &sA[s & 1][lk * 16 + lc];
+#pragma unroll
+                for (int gq = 0; gq < G; gq++) {
+#pragma unroll
+                    for (int b = 0; b < SB; b++) {
+                        const double a = sa[b * KMAX * 16 + gq * 64];
+                        ae[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, be[gq], ae[b], 0, 0, 0);
+                        ao[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bo[gq], ao[b], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int b = 0; b < SB; b++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int64_t row = i0 + (int64_t)s * STEP + 16 * b + lk + 4 * r;
+                        if (ok && row < i1)
+                            __builtin_nontemporal_store(d2{ae[b][r], ao[b][r]}, (d2 *)(T + row * ld + cl));
+                    }
             }
 #pragma unroll
-            for (int r = 0; r < 4; r++) t[r] = tn[r];
+            for (int b = 0; b < SB; b++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) t[b][r] = tn[b][r];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
+}
+
+
+// k_flushy: roles swapped against k_flushw. A block stages the negated P of
+// a 64-column tile (all KMAX slots, padded rows) in LDS once per item; each
+// wave then sweeps its own 16-row bands (wave w: bands w, w+4, ...) with no
+// block barrier: A fragments (raw C of the band's 16 rows, 32 doubles per
+// lane at KMAX = 128) in VGPRs, B from LDS (one ds_read_b128 feeds the even-
+// and odd-column tiles), four independent MFMA chains per wave (two 32-column
+// halves x even/odd), the next band's A and tableau loads issued before the
+// current band's MFMAs (PF = 1).
+template <int KMAX, int LB, int PF, int MODE = 0>
+__global__ __launch_bounds__(256, LB) void k_flushy(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                    const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
+                                                    int64_t cs, int64_t ntiles, int64_t nitems, int64_t rows, int skip) {
+    constexpr int G = KMAX / 4;
+    constexpr int PS = 68;                        // padded LDS row (doubles): rows lk = 0..3 start on different banks
+    constexpr int SU = KMAX * 32 / 256;           // 16-byte P pieces staged per thread
+    __shared__ __attribute__((aligned(16))) double sP[KMAX * PS];
+    __shared__ int64_t next_item;
+    __shared__ unsigned lmask;
+    const int np = (int)st->npend;
+    if (np <= 0) return;
+    const int64_t ld = g.ld;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lc = lane & 15, lk = lane >> 4;
+    unsigned long long touched = 0;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
+            lmask = 0;
+        }
+        __syncthreads();
+        const int64_t item = next_item;
+        if (item >= nitems) break;
+        const int64_t tile = item % ntiles, strip = item / ntiles;
+        const int64_t i0 = strip * rows;
+        const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
+        const int64_t c0 = tile * 64;
+        {   // stage -P: piece e = (q, pair cp), cp = e % 32 is the same for all of this thread's pieces
+            const int cp = threadIdx.x & 31;
+            const int64_t cj = c0 + 2 * cp;
+            bool lv = false;
+#pragma unroll
+            for (int u = 0; u < SU; u++) {
+                const int q = (u * 256 + threadIdx.x) >> 5;
+                d2 v = d2{0.0, 0.0};
+                if (q < np && cj < g.ncols) v = *(const d2 *)(Pbuf + (int64_t)q * ld + cj);
+                lv = lv || v.x != 0.0 || v.y != 0.0;
+                *(d2 *)&sP[q * PS + 2 * cp] = -v;
+            }
+            if (lv) atomicOr(&lmask, 1u << cp);
+        }
+        __syncthreads();
+        const unsigned lm = lmask;
+        if (lm == 0 && skip) continue;                            // the whole tile is skipped
+        const unsigned live = skip ? lm : 0xffffffffu;
+        bool okh[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) okh[h] = ((live >> (16 * h + lc)) & 1u) && c0 + 32 * h + 2 * lc < g.ncols;
+        if (threadIdx.x == 0) {
+            unsigned long long cols = 0;
+            for (int cp = 0; cp < 32; cp++)
+                if (((live >> cp) & 1u) && c0 + 2 * cp < g.ncols) cols += (c0 + 2 * cp + 1 < g.ncols) ? 2 : 1;
+            touched += cols * (unsigned long long)(i1 - i0);
+        }
+        const int nb = (int)((i1 - i0 + 15) / 16);
+        auto aload = [&](double (&a)[G], int b) {
+            const int64_t row = i0 + 16 * (int64_t)b + lc;
+#pragma unroll
+            for (int gq = 0; gq < G; gq++) {
+                const int q = 4 * gq + lk;
+                a[gq] = q < np ? Cbuf[(int64_t)q * cs + row] : 0.0;
+            }
+        };
+        auto tload = [&](d2 (&x)[2][4], int b) {
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = i0 + 16 * (int64_t)b + lk + 4 * r;
+                    x[h][r] = (MODE != 2 && okh[h] && row < i1)
+                                  ? __builtin_nontemporal_load((const d2 *)(T + row * ld + c0 + 32 * h + 2 * lc))
+                                  : d2{0.0, 0.0};
+                }
+        };
+        int b = wave;
+        if (b >= nb) continue;
+        double a[G];
+        d2 t[2][4];
+        aload(a, b);
+        tload(t, b);
+        for (; b < nb; b += 4) {
+            double an[G];
+            d2 tn[2][4];
+            const bool more = PF && b + 4 < nb;
+            if (more) {
+                aload(an, b + 4);
+                tload(tn, b + 4);
+            }
+            d4 acc[4];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                acc[2 * h] = d4{t[h][0].x, t[h][1].x, t[h][2].x, t[h][3].x};
+                acc[2 * h + 1] = d4{t[h][0].y, t[h][1].y, t[h][2].y, t[h][3].y};
+            }
+            const double *sp = &sP[lk * PS + 2 * lc];
+            // B of step gq + 1 is read from LDS before the MFMAs of step gq (two register sets), so
+            // the LDS latency hides behind four MFMAs instead of stalling every step
+            d2 b0c = *(const d2 *)sp, b1c = *(const d2 *)(sp + 32);
+#pragma unroll
+            for (int gq = 0; gq < (MODE == 1 ? 0 : G); gq++) {
+                d2 b0n = b0c, b1n = b1c;
+                if (gq + 1 < G) {
+                    b0n = *(const d2 *)(sp + 4 * (gq + 1) * PS);
+                    b1n = *(const d2 *)(sp + 4 * (gq + 1) * PS + 32);
+                }
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[gq], b0c.x, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[gq], b0c.y, acc[1], 0, 0, 0);
+                acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[gq], b1c.x, acc[2], 0, 0, 0);
+                acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[gq], b1c.y, acc[3], 0, 0, 0);
+                b0c = b0n;
+                b1c = b1n;
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the 2 LDS reads of step gq + 1 ...
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // ... ahead of the 4 MFMAs of step gq
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = i0 + 16 * (int64_t)b + lk + 4 * r;
+                    if ((MODE != 2 || acc[2 * h][r] == 12345.0) && okh[h] && row < i1)
+                        __builtin_nontemporal_store(d2{acc[2 * h][r], acc[2 * h + 1][r]},
+                                                    (d2 *)(T + row * ld + c0 + 32 * h + 2 * lc));
+                }
+            if (!PF && b + 4 < nb) {
+                aload(an, b + 4);
+                tload(tn, b + 4);
+            }
+#pragma unroll
+            for (int gq = 0; gq < G; gq++) a[gq] = an[gq];
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) t[h][r] = tn[h][r];
         }
     }
     if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
@@ -262,18 +323,14 @@ __global__ void k_fill(double *x, int64_t n, uint64_t seed) {
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
         z ^= z >> 31;
-        x[i] = (double)(z >> 11) * 0x1.0p-53;
+        x[i] = (double)(z >> 11) * 0x1.0p-53 - 0.25;
     }
 }
 
-// P_q[j] = 0 for the slack block and the padding (the skipped columns),
-// except every `every`-th slack column (0: none), which stays live: the
-// slacks that left the basis, scattered over the block as in a real solve
-__global__ void k_zero_cols(double *P, int64_t ld, int64_t j0, int64_t j1, int k, int64_t every) {
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)k * ld; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t j = e % ld;
-        if (j >= j0 && !(every > 0 && j < j1 && (j - j0) % every == 0)) P[e] = 0.0;
-    }
+// P_q[j] = 0 for the slack block and the padding (the skipped columns)
+__global__ void k_zero_cols(double *P, int64_t ld, int64_t j0, int k) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)k * ld; e += (int64_t)gridDim.x * blockDim.x)
+        if (e % ld >= j0) P[e] = 0.0;
 }
 
 __global__ void k_cmp(const double *a, const double *b, int64_t n, unsigned long long *bad) {
@@ -285,43 +342,78 @@ __global__ void k_cmp(const double *a, const double *b, int64_t n, unsigned long
 
 struct Lab {
     Geo g{};
-    Defer D{};
     DevState *st = nullptr;
-    double *T = nullptr, *T0 = nullptr, *Tref = nullptr;
-    int64_t n = 0;
-    int K = 32;
+    double *T = nullptr, *T0 = nullptr, *Tref = nullptr, *Pbuf = nullptr, *Cbuf = nullptr, *zbuf = nullptr;
+    int64_t n = 0, cs = 0;
+    int K = 128;
     unsigned long long *bad = nullptr;
     hipEvent_t e0, e1;
 
-    void reset_state() {
+    void reset_state(int np) {
         DevState h{};
-        h.npend = K;
-        h.fwork = 0;
+        h.npend = np;
         CHK(hipMemcpy(st, &h, sizeof h, hipMemcpyHostToDevice));
     }
 };
 
 typedef void (*LaunchFn)(Lab &L);
 
-static double run(Lab &L, LaunchFn fn, const char *name, bool check, int reps) {
-    if (check) {
-        CHK(hipMemcpy(L.T, L.T0, L.n * 8, hipMemcpyDeviceToDevice));
-        L.reset_state();
-        fn(L);
-        CHK(hipGetLastError());
-        CHK(hipDeviceSynchronize());
-        CHK(hipMemset(L.bad, 0, 8));
-        hipLaunchKernelGGL(k_cmp, dim3(4096), dim3(256), 0, 0, L.T, L.Tref, L.n, L.bad);
-        unsigned long long nb = 0;
-        CHK(hipMemcpy(&nb, L.bad, 8, hipMemcpyDeviceToHost));
-        if (nb) {
-            printf("%-34s MISMATCH: %llu doubles differ from the engine flush\n", name, nb);
-            return -1;
-        }
+// the engine's k_flushw<64> twice: slots 0..63, then 64..127 (same chain)
+static void fn_ref(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 127) / 128;
+    const int64_t rows = 512, nitems = ntiles * ((L.g.nloc + rows - 1) / rows);
+    for (int h = 0; h < L.K / 64; h++) {
+        L.reset_state(64);
+        hipLaunchKernelGGL((k_flushw<64, 2, 2, 4>), dim3(512), dim3(256), 0, 0, L.g.T, L.g, L.st,
+                           L.Pbuf + (int64_t)h * 64 * L.g.ld, L.Cbuf + (int64_t)h * 64 * L.cs, L.cs, ntiles, nitems,
+                           rows, 1);
+    }
+}
+
+template <int KMAX, int NB, int LB, int R>
+static void fn_w(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 127) / 128;
+    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
+    L.reset_state(L.K);
+    hipLaunchKernelGGL((k_flushw<KMAX, NB, LB, 4>), dim3((unsigned)std::min<int64_t>(nitems, 256 * LB)), dim3(256), 0,
+                       0, L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, (int64_t)R, 1);
+}
+
+template <int KMAX, int SB, int LB, int R>
+static void fn_x(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 127) / 128;
+    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
+    L.reset_state(L.K);
+    hipLaunchKernelGGL((k_flushx<KMAX, SB, LB>), dim3((unsigned)std::min<int64_t>(nitems, 256 * LB)), dim3(256), 0, 0,
+                       L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, (int64_t)R, 1, L.zbuf);
+}
+
+template <int KMAX, int LB, int PF, int R, int MODE = 0>
+static void fn_y(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 63) / 64;
+    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
+    L.reset_state(L.K);
+    hipLaunchKernelGGL((k_flushy<KMAX, LB, PF, MODE>), dim3((unsigned)std::min<int64_t>(nitems, 256 * LB)), dim3(256), 0, 0,
+                       L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, (int64_t)R, 1);
+}
+
+static bool g_nocheck = false;
+static double run(Lab &L, LaunchFn fn, const char *name, int reps) {
+    CHK(hipMemcpy(L.T, L.T0, L.n * 8, hipMemcpyDeviceToDevice));
+    fn(L);
+    CHK(hipGetLastError());
+    CHK(hipDeviceSynchronize());
+    CHK(hipMemset(L.bad, 0, 8));
+    hipLaunchKernelGGL(k_cmp, dim3(4096), dim3(256), 0, 0, L.T, L.Tref, L.n, L.bad);
+    unsigned long long nb = 0;
+    CHK(hipMemcpy(&nb, L.bad, 8, hipMemcpyDeviceToHost));
+    if (nb && !g_nocheck) {
+        printf("%-28s MISMATCH: %llu doubles differ from the reference\n", name, nb);
+        fflush(stdout);
+        return -1;
     }
     double best = 1e30, sum = 0;
     for (int r = 0; r < reps; r++) {
-        L.reset_state();
         CHK(hipEventRecord(L.e0));
         fn(L);
         CHK(hipEventRecord(L.e1));
@@ -334,72 +426,33 @@ static double run(Lab &L, LaunchFn fn, const char *name, bool check, int reps) {
     DevState h{};
     CHK(hipMemcpy(&h, L.st, sizeof h, hipMemcpyDeviceToHost));
     const double bytes = 16.0 * (double)h.touched;
-    printf("%-34s K=%d  best %.3f ms  mean %.3f ms  touched %.3f GB  %.0f GB/s (best)\n", name, L.K, best, sum / reps,
-           bytes / 1e9, bytes / (best * 1e-3) / 1e9);
+    const double flops = 2.0 * L.K * (double)h.touched;
+    printf("%-28s K=%d  best %.3f ms  mean %.3f ms  touched %.3f GB  %.0f GB/s  %.1f TFLOP/s (best)\n", name, L.K,
+           best, sum / reps, bytes / 1e9, bytes / (best * 1e-3) / 1e9, flops / (best * 1e-3) / 1e12);
     fflush(stdout);
     return best;
 }
 
-static int g_variant = 8;
-static void fn_engine(Lab &L) {
-    Launch la{nullptr};
-    if (launch_flush(la, L.g, L.st, L.D, L.K, 1, g_variant)) {
-        printf("launch_flush failed\n");
-        exit(1);
-    }
-}
-
-template <int KMAX, int SR, int NSUB, int PERCU>
-static void fn_r(Lab &L) {
-    const int64_t ntiles = (L.g.ncols + 63) / 64;
-    const int64_t nitems = ntiles * ((L.g.nloc + SR - 1) / SR);
-    const int64_t nblocks = std::min<int64_t>(nitems, 256 * PERCU);
-    hipLaunchKernelGGL((k_flushr<KMAX, SR, NSUB>), dim3((unsigned)nblocks), dim3(kBlock), 0, 0, L.g.T, L.g, L.st,
-                       L.D.Pbuf, L.D.Cbuf, L.D.cs, ntiles, nitems, 1);
-}
-
-template <int KMAX, int R, int NB, int LB, int PERCU>
-static void fn_w(Lab &L) {
-    const int64_t ntiles = (L.g.ncols + 127) / 128;
-    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
-    const int64_t nblocks = std::min<int64_t>(nitems, 256 * PERCU);
-    hipLaunchKernelGGL((k_flushw<KMAX, NB, LB>), dim3((unsigned)nblocks), dim3(kBlock), 0, 0, L.g.T, L.g, L.st,
-                       L.D.Pbuf, L.D.Cbuf, L.D.cs, ntiles, nitems, (int64_t)R, 1);
-}
-
-template <int KMAX, int R, int NB, int LB, int PERCU>
-static void fn_w2(Lab &L) {
-    const int64_t ntiles = (L.g.ncols + 127) / 128;
-    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
-    const int64_t nblocks = std::min<int64_t>(nitems, 256 * PERCU);
-    hipLaunchKernelGGL((k_flushw2<KMAX, NB, LB>), dim3((unsigned)nblocks), dim3(kBlock), 0, 0, L.g.T, L.g, L.st,
-                       L.D.Pbuf, L.D.Cbuf, L.D.cs, ntiles, nitems, (int64_t)R, 1);
-}
-
 int main(int argc, char **argv) {
     Lab L;
-    L.K = argc > 1 ? atoi(argv[1]) : 32;
-    const int64_t m = argc > 2 ? atoll(argv[2]) : 16384, nstruct = 2 * m;
+    const int64_t m = argc > 1 ? atoll(argv[1]) : 16384, nstruct = 2 * m;
     const int64_t ncols = nstruct + m + 1, ld = (ncols + 63) / 64 * 64;
     L.n = m * ld;
+    L.cs = (m + 63) / 64 * 64;
+    const int SL = 128;
     CHK(hipMalloc(&L.T, L.n * 8));
     CHK(hipMalloc(&L.T0, L.n * 8));
     CHK(hipMalloc(&L.Tref, L.n * 8));
     CHK(hipMalloc(&L.st, sizeof(DevState)));
     CHK(hipMalloc(&L.bad, 8));
-    double *Pbuf, *Cbuf;
-    int64_t *rq;
-    const int64_t cs = (m + 63) / 64 * 64;
-    const int SL = 128;                                  // slots (blocks up to 128 pivots)
-    CHK(hipMalloc(&Pbuf, (size_t)SL * ld * 8));
-    CHK(hipMalloc(&Cbuf, (size_t)SL * cs * 8));
-    CHK(hipMalloc(&rq, SL * 8));
-    CHK(hipMemset(rq, 0xff, SL * 8));                 // -1: no pivot row of the block is local
+    CHK(hipMalloc(&L.Pbuf, (size_t)SL * ld * 8));
+    CHK(hipMalloc(&L.Cbuf, (size_t)SL * L.cs * 8));
+    CHK(hipMalloc(&L.zbuf, 4096));
+    CHK(hipMemset(L.zbuf, 0, 4096));
     hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, L.T0, L.n, 1ull);
-    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, Pbuf, (int64_t)SL * ld, 2ull);
-    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, Cbuf, (int64_t)SL * cs, 3ull);
-    const int64_t every = getenv("LAB_SCATTER") ? atoll(getenv("LAB_SCATTER")) : 0;
-    hipLaunchKernelGGL(k_zero_cols, dim3(1024), dim3(256), 0, 0, Pbuf, ld, nstruct + 1, ncols, SL, every);
+    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, L.Pbuf, (int64_t)SL * ld, 2ull);
+    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, L.Cbuf, (int64_t)SL * L.cs, 3ull);
+    hipLaunchKernelGGL(k_zero_cols, dim3(1024), dim3(256), 0, 0, L.Pbuf, ld, nstruct + 1, SL);
     CHK(hipDeviceSynchronize());
     L.g.T = L.T;
     L.g.ld = ld;
@@ -408,54 +461,29 @@ int main(int argc, char **argv) {
     L.g.ncols = ncols;
     L.g.nact = ncols - 1;
     L.g.m = m;
-    L.D.Pbuf = Pbuf;
-    L.D.Cbuf = Cbuf;
-    L.D.cs = cs;
-    L.D.rq = rq;
-    CHK(hipMalloc(&L.D.mul, (size_t)LPG_DEFER_MAX * LPG_DEFER_MAX * 8));
-    L.D.on = 1;
     CHK(hipEventCreate(&L.e0));
     CHK(hipEventCreate(&L.e1));
-    printf("flush lab: %lld rows x %lld cols (ld %lld), K=%d, P zero for columns > %lld except every %lld-th\n",
-           (long long)m, (long long)ncols, (long long)ld, L.K, (long long)nstruct, (long long)every);
+    printf("flush lab: %lld rows x %lld cols (ld %lld), K=%d, P zero for columns > %lld\n", (long long)m,
+           (long long)ncols, (long long)ld, L.K, (long long)nstruct);
+    CHK(hipMemcpy(L.T, L.T0, L.n * 8, hipMemcpyDeviceToDevice));
+    fn_ref(L);
+    CHK(hipDeviceSynchronize());
+    CHK(hipMemcpy(L.Tref, L.T, L.n * 8, hipMemcpyDeviceToDevice));
     const int reps = 5;
     const char *only = getenv("LAB_ONLY");
     auto want = [&](const char *nm) { return !only || strstr(nm, only); };
-    if (L.K > 64) {   // beyond the engine's blocks: timing only (no reference flush to compare with)
-#define WB(KM, R, NB, LB, PC)                                                                      \
-        if (L.K <= KM && want("w<" #KM "," #R "," #NB "," #LB "," #PC ">"))                        \
-            run(L, fn_w<KM, R, NB, LB, PC>, "w<" #KM "," #R "," #NB "," #LB "," #PC ">", false, reps);
-        WB(96, 512, 2, 2, 2) WB(96, 512, 2, 1, 1) WB(128, 512, 2, 1, 1) WB(128, 512, 2, 2, 2) WB(128, 1024, 2, 1, 1)
-        return 0;
-    }
-    // reference result: the engine's default flush
-    CHK(hipMemcpy(L.T, L.T0, L.n * 8, hipMemcpyDeviceToDevice));
-    L.reset_state();
-    fn_engine(L);
-    CHK(hipDeviceSynchronize());
-    CHK(hipMemcpy(L.Tref, L.T, L.n * 8, hipMemcpyDeviceToDevice));
-    for (int v : {8, 19, 20, 14, 16}) {
-        g_variant = v;
-        char nm[64];
-        snprintf(nm, sizeof nm, "engine variant %d", v);
-        if (want(nm)) run(L, fn_engine, nm, true, reps);
-    }
-#define R(KM, SR, NS, PC)                                                       \
-    if (L.K <= KM && want("r<" #KM "," #SR "," #NS "," #PC ">"))               \
-        run(L, fn_r<KM, SR, NS, PC>, "r<" #KM "," #SR "," #NS "," #PC ">", true, reps);
-    if (L.K <= 32) {
-        R(32, 64, 1, 4) R(32, 64, 2, 4) R(32, 128, 2, 4) R(32, 64, 4, 4) R(32, 128, 4, 2)
-    } else {
-        R(64, 64, 1, 4) R(64, 64, 2, 4) R(64, 32, 2, 6) R(64, 64, 4, 4) R(64, 32, 1, 6)
-    }
-#define W(KM, R, NB, LB, PC)                                                            \
-    if (L.K <= KM && want("w<" #KM "," #R "," #NB "," #LB "," #PC ">"))                  \
-        run(L, fn_w<KM, R, NB, LB, PC>, "w<" #KM "," #R "," #NB "," #LB "," #PC ">", true, reps);
-    if (L.K <= 32) {
-        W(32, 512, 2, 3, 3) W(32, 512, 3, 3, 3) W(32, 256, 2, 3, 3) W(32, 1024, 2, 3, 3) W(32, 512, 2, 4, 4)
-    } else {
-        W(64, 512, 2, 2, 2) W(64, 512, 3, 2, 2) W(64, 256, 2, 2, 2) W(64, 1024, 2, 2, 2)
-    }
-    if (L.K > 32 && want("w2<64,512,2,2,2>")) run(L, fn_w2<64, 512, 2, 2, 2>, "w2<64,512,2,2,2>", true, reps);
+    if (want("ref 2x w<64>")) run(L, fn_ref, "ref 2x w<64>", reps);
+#define W(KM, NB, LB, R) \
+    if (want("w<" #KM "," #NB "," #LB "," #R ">")) run(L, fn_w<KM, NB, LB, R>, "w<" #KM "," #NB "," #LB "," #R ">", reps);
+#define X(KM, SB, LB, R) \
+    if (want("x<" #KM "," #SB "," #LB "," #R ">")) run(L, fn_x<KM, SB, LB, R>, "x<" #KM "," #SB "," #LB "," #R ">", reps);
+    W(128, 2, 1, 512)
+    X(128, 2, 1, 512)
+#define Y(KM, LB, PF, R) \
+    if (want("y<" #KM "," #LB "," #PF "," #R ">")) run(L, fn_y<KM, LB, PF, R>, "y<" #KM "," #LB "," #PF "," #R ">", reps);
+    Y(128, 1, 1, 2048)
+    g_nocheck = true;   // timing-only probes: no MFMA (memory alone), no tableau traffic (matrix cores alone)
+    if (want("ymem")) run(L, fn_y<128, 1, 1, 2048, 1>, "ymem<128> (no MFMA)", reps);
+    if (want("ymfma")) run(L, fn_y<128, 1, 1, 2048, 2>, "ymfma<128> (no T traffic)", reps);
     return 0;
 }

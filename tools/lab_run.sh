@@ -1,3 +1,5 @@
+#!/bin/bash
+# flush lab on the GPU box (tools/flush_lab.hip): config-3 rows, then config-4-like rows
 set -u
-timeout -k 10 120 tools/flush_lab 96 > gpurun_out/lab96.log 2>&1 || exit $?
-timeout -k 10 120 tools/flush_lab 128 > gpurun_out/lab128.log 2>&1 || exit $?
+mkdir -p gpurun_out
+timeout -k 10 300 ./tools/flush_lab ${LAB_ROWS:-16384} > gpurun_out/flush_lab.log 2>&1 || exit $?
