@@ -81,6 +81,7 @@ struct lpg_ctx {
     int64_t *kq = nullptr, *lv = nullptr;   // per pending pivot: entering / leaving variable
     int32_t *colmap = nullptr, *inv = nullptr, *pairs = nullptr;
     double *mul = nullptr;        // pivot-row multipliers of a flush (LPG_DEFER_MAX^2)
+    double *pv = nullptr;         // pivot elements of the pending block (replicated)
     double *tmp = nullptr;        // row chunk for canonicalize()
     int64_t tmp_rows = 0;
     bool permuted = false;        // colmap may differ from the identity
@@ -280,6 +281,7 @@ static Defer defer_of(const lpg_ctx *c, int q) {
     d.colmap = c->colmap;
     d.inv = c->inv;
     d.mul = c->mul;
+    d.pv = c->pv;
     d.q = q;
     d.on = c->defer_k > 0 ? 1 : 0;
     return d;
@@ -288,7 +290,11 @@ static Defer defer_of(const lpg_ctx *c, int q) {
 // Apply the pending block (its size on the device is st->npend <= pend).
 // In deferred mode the timing ring brackets exactly this (k_flush +
 // k_flush_pivot_rows + the counter reset).
-static bool reorders(const lpg_ctx *c) { return c->defer_k > 0 && c->fast_pivot && !has_comm(c) && c->colmap; }
+// Reordered columns need the prefetching pivot pair (k_prep_d / k_select_d;
+// with a communicator k_price mode 1 between them prices logical keys): every
+// rank runs the same plan from replicated data (kq, lv, pv), so the physical
+// order, and with it the exchanged P, is the same on every rank.
+static bool reorders(const lpg_ctx *c) { return c->defer_k > 0 && c->fast_pivot && c->colmap; }
 
 // The timing ring brackets the block pass alone (k_flushw / k_flushm), the
 // kernel the roofline reports; the swap plan, pivot-row rewrite and column
@@ -513,7 +519,7 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
             if (launch_prep_dm(L, g, rule, c->st, s, c->cand, ncand_d, P, c->C[s], c->npp_d, D))
                 return fail(c, LPG_ERR_DEVICE, "prep launch failed");
             if ((rc = comm_allreduce_sum(c, P, (size_t)c->ld))) return rc;
-            if (launch_price(L, g, rule, 1, c->st, s, P, c->C[s], c->pp, c->pc, c->npp, true))
+            if (launch_price(L, g, rule, 1, c->st, s, P, c->C[s], c->pp, c->pc, c->npp, true, c->colmap, c->inv))
                 return fail(c, LPG_ERR_DEVICE, "price launch failed");
             if (launch_select_dm(L, g, rule, c->st, s, s1, c->C[s], c->C[s1], c->pp, c->npp, c->basis, c->part,
                                  c->nsel_d, D))
@@ -723,6 +729,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         ALLOC(c->inv, (size_t)c->ld * sizeof(int32_t));
         ALLOC(c->pairs, (size_t)(1 + 3 * 64) * sizeof(int32_t));
         ALLOC(c->mul, (size_t)LPG_DEFER_MAX * LPG_DEFER_MAX * sizeof(double));
+        ALLOC(c->pv, (size_t)slots * sizeof(double));
     }
 #undef ALLOC
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -814,7 +821,7 @@ void lpg_destroy(lpg_ctx *c) {
     for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
-                    c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->mul, c->tmp};
+                    c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->mul, c->pv, c->tmp};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);

@@ -65,6 +65,7 @@ struct Defer {
     const int32_t *colmap;    // ld: logical column held by physical column p (k_prep_d's pricing keys)
     const int32_t *inv;       // ld: physical column of logical column j (k_select_d when npp > its block)
     double  *mul;             // K x K: -C_u[r_q] (k_flush_pivot_rows' multipliers, built by k_swap_plan)
+    double  *pv;              // K: pivot element of pending pivot q (replicated on every rank; k_swap_plan)
     int      q;               // pending index of this pivot
     int      on;
 };
@@ -110,7 +111,8 @@ int launch_generate(const Launch &L, const Geo &g, int64_t n, uint64_t seed, int
 int launch_objective_chain(const Launch &L, const Geo &g, const double *cb, const double *acc_in, double *acc_out);
 int launch_objective_finish(const Launch &L, const Geo &g, const double *acc, const double *cost, int64_t orow);
 int launch_price(const Launch &L, const Geo &g, int rule, int mode, const DevState *st, int s,
-                 const double *P, const double *Cs, PricePart *pp, int *pc, int npp, bool defer = false);
+                 const double *P, const double *Cs, PricePart *pp, int *pc, int npp, bool defer = false,
+                 const int32_t *colmap = nullptr, const int32_t *inv = nullptr);
 int launch_prep(const Launch &L, const Geo &g, int rule, bool fuse_price, DevState *st, int s,
                 const Cand *cand, int ncand, double *P, const double *Cs, PricePart *pp, int *pc, int npp,
                 const Defer &D);
@@ -155,7 +157,7 @@ int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0:
 // launch_fill_cols (after the pivot-row rewrite) writes the entering
 // columns' unit vectors (lpg_kernels.hip, above k_swap_plan).
 int launch_swap_plan(const Launch &L, const DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
-                     int32_t *pairs, int plan);
+                     int32_t *pairs, int plan);   // reads D.pv (replicated pivot elements)
 int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs);
 int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs);
 // Canonical order again: rows [i0, i0 + nr) gathered through inv into tmp

@@ -410,11 +410,15 @@ __device__ __forceinline__ void count_live(int *__restrict__ pc, bool live) {
     if (threadIdx.x == 0) pc[blockIdx.x] = n;
 }
 
+// colmap / inv (deferred multi-rank path with reordered columns, lpg_internal.h):
+// the pricing keys are logical (colmap of the physical column), as in
+// k_prep_d; the block winner's physical column comes back through inv.
 template <int RULE, int MODE>
 __global__ __launch_bounds__(kBlock) void k_price(double *__restrict__ T, Geo g,
                                                   const DevState *__restrict__ st, int s,
                                                   const double *__restrict__ P, const double *__restrict__ Cs,
-                                                  PricePart *__restrict__ pp, int *__restrict__ pc, int defer) {
+                                                  PricePart *__restrict__ pp, int *__restrict__ pc, int defer,
+                                                  const int32_t *__restrict__ colmap, const int32_t *__restrict__ inv) {
     if (MODE == 1 && st->slot[s].status != RUNNING) return;
     const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t nvec = (g.ncols + 1) / 2;
@@ -437,8 +441,9 @@ __global__ __launch_bounds__(kBlock) void k_price(double *__restrict__ T, Geo g,
                 if (g.nobj == 2) *(d2 *)(T + rM * g.ld + 2 * j2) = dM;
             }
         }
-        price_one<RULE>(best, dM.x, dR.x, 2 * j2, g);
-        price_one<RULE>(best, dM.y, dR.y, 2 * j2 + 1, g);
+        const int2 lj = colmap ? ((const int2 *)colmap)[j2] : int2{(int)(2 * j2), (int)(2 * j2 + 1)};
+        price_one<RULE>(best, dM.x, dR.x, lj.x, g);
+        price_one<RULE>(best, dM.y, dR.y, lj.y, g);
     }
     if (MODE == 1) count_live(pc, live);
     best = block_reduce_pp<RULE>(best);
@@ -447,21 +452,24 @@ __global__ __launch_bounds__(kBlock) void k_price(double *__restrict__ T, Geo g,
     // "if (better) best = c" in this kernel (pad kept the previous best's
     // value while v, j, cls took the new one), which sent k_select_d to the
     // neighbouring column under a communicator.
-    best.pad = (int32_t)best.j;
-    if (threadIdx.x == 0) pp[blockIdx.x] = best;
+    if (threadIdx.x == 0) {
+        best.pad = (int32_t)(best.j >= 0 && inv ? inv[best.j] : best.j);
+        pp[blockIdx.x] = best;
+    }
 }
 
 int launch_price(const Launch &L, const Geo &g, int rule, int mode, const DevState *st, int s,
-                 const double *P, const double *Cs, PricePart *pp, int *pc, int npp, bool defer) {
+                 const double *P, const double *Cs, PricePart *pp, int *pc, int npp, bool defer,
+                 const int32_t *colmap, const int32_t *inv) {
     hipStream_t stream = (hipStream_t)L.stream;
     dim3 grid(npp), blk(kBlock);
     const int d = defer ? 1 : 0;
     if (rule == RULE_BLAND) {
-        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_BLAND, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d);
-        else hipLaunchKernelGGL((k_price<RULE_BLAND, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d);
+        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_BLAND, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d, colmap, inv);
+        else hipLaunchKernelGGL((k_price<RULE_BLAND, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d, colmap, inv);
     } else {
-        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_DANTZIG, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d);
-        else hipLaunchKernelGGL((k_price<RULE_DANTZIG, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d);
+        if (mode == 0) hipLaunchKernelGGL((k_price<RULE_DANTZIG, 0>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d, colmap, inv);
+        else hipLaunchKernelGGL((k_price<RULE_DANTZIG, 1>), grid, blk, 0, stream, g.T, g, st, s, P, Cs, pp, pc, d, colmap, inv);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -886,6 +894,7 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
         st->npend = D.q + 1;
         D.kq[D.q] = k;                       // entering and leaving variables of the block (k_swap_plan)
         D.lv[D.q] = D.basis[best.row];
+        D.pv[D.q] = best.piv;                // pivot element, known to every rank (k_swap_plan)
         D.basis[best.row] = k;
         const int64_t n = st->pivots;
         if (D.logk && n < st->logcap) {
@@ -2038,7 +2047,8 @@ __global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ s
                                                   const int64_t *__restrict__ lv, const int64_t *__restrict__ rq,
                                                   const double *__restrict__ Cbuf, int64_t cs,
                                                   int32_t *__restrict__ colmap, int32_t *__restrict__ inv,
-                                                  int32_t *__restrict__ pairs, double *__restrict__ mul, int plan) {
+                                                  int32_t *__restrict__ pairs, double *__restrict__ mul, int plan,
+                                                  const double *__restrict__ pv) {
     const int np = (int)st->npend;
     if (blockIdx.x > 0) {                                   // mul[u][q], lane q
         constexpr int UB = LPG_DEFER_MAX / kMulBlocks;       // pivots u per block
@@ -2059,8 +2069,9 @@ __global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ s
     if (!plan) return;
     const int q = threadIdx.x;
     const int64_t x = q < np ? kq[q] : -1, y = q < np ? lv[q] : -1, rx = q < np ? rq[q] : -1;
-    // pivot element of pivot q: C_q[r_q]
-    const bool pos = q >= np || (rx >= 0 && Cbuf[(int64_t)q * cs + rx] > 0.0);
+    // pivot element of pivot q (C_q[r_q], recorded by k_prep_d on every rank, so that every rank of a
+    // row partition -- most of which do not hold row r_q -- makes the same plan)
+    const bool pos = q >= np || pv[q] > 0.0;
     // x (entering at q) is in E iff no later event touches x and its first event is an entry
     bool inE = q < np, inL = q < np;
     int fx = q, fy = q;           // first event index of x / y, and its kind
@@ -2164,7 +2175,7 @@ __global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Ge
 int launch_swap_plan(const Launch &L, const DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
                      int32_t *pairs, int plan) {
     hipLaunchKernelGGL(k_swap_plan, dim3(1 + kMulBlocks), dim3(64), 0, (hipStream_t)L.stream, st, D.kq, D.lv, D.rq,
-                       D.Cbuf, D.cs, colmap, inv, pairs, D.mul, plan);
+                       D.Cbuf, D.cs, colmap, inv, pairs, D.mul, plan, D.pv);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
