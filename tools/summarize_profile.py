@@ -32,7 +32,7 @@ def _one(pattern):
 
 
 def short(name: str) -> str:
-    for key in ("k_flush_pivot_rows", "k_swap_plan", "k_move_cols", "k_fill_cols", "k_flush", "k_update", "k_select", "k_prep", "k_price", "k_generate", "k_basis_slack", "k_objective"):
+    for key in ("k_flush_pivot_rows", "k_swap_plan", "k_move_cols", "k_fill_cols", "k_flushw", "k_flushm", "k_update", "k_select_d", "k_prep_d", "k_select", "k_prep", "k_price", "k_generate", "k_basis_slack", "k_objective"):
         if key in name:
             return key
     return name[:60]
@@ -69,8 +69,10 @@ def main():
         out["FETCH_SIZE"] = counter_means(fetch, "FETCH_SIZE")
     if write:
         out["WRITE_SIZE"] = counter_means(write, "WRITE_SIZE")
-    # dominant kernel: the deferred block flush if it ran, else the eager update
-    kern = "k_flush" if fetch and "k_flush" in out.get("FETCH_SIZE", {}) else "k_update"
+    # dominant kernel: the deferred block pass if it ran (k_flushw for 64-pivot blocks), else the eager update
+    fk = out.get("FETCH_SIZE", {})
+    kern = "k_flushw" if "k_flushw" in fk else ("k_flushm" if "k_flushm" in fk else "k_update")
+    pending = int(os.environ.get("PENDING", "64"))
     # FETCH_SIZE correction: x2 for 16-B/lane streaming reads (guide); other widths
     # are calibrated with tools/hbm_calib3 (--fetch-factor F)
     ff = float(os.environ.get("FETCH_FACTOR", "2.0"))
@@ -89,7 +91,9 @@ def main():
     if upd is not None:
         with open(os.path.join(ROOT, "profiles", f"pmc_config{cfg}.json"), "w") as f:
             json.dump({"hbm_bytes_per_launch": upd, "source": f"profiles/r{rnd:02d}_pmc.json",
-                       "kernel": f"lpg::{kern}", "fetch_factor": ff}, f, indent=1)
+                       "kernel": kern, "pending_pivots": pending, "fetch_factor": ff,
+                       "how": "tools/profile.sh: separate rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of "
+                              "bench.py (whole 64-pivot blocks, no warm-up), means over the block passes"}, f, indent=1)
     print(json.dumps(out, indent=1))
 
 
