@@ -1,4 +1,4 @@
-"""Row-block partition protocol, world_size 2 and 3, torch.distributed `gloo` on CPU.
+"""Row-block partition protocol, world_size 2, 3, 4 and 8, torch.distributed `gloo` on CPU.
 
 The multi-GPU engine (linearprogramming_amd/csrc/lpg_ctx.hip, `enqueue`)
 exchanges exactly two things per pivot: the ratio-test candidates
@@ -75,6 +75,9 @@ def _free_port():
     (2, 40, 64, GEN_DENSE, RULE_DANTZIG),
     (2, 33, 50, GEN_DEGENERATE, RULE_BLAND),
     (3, 47, 61, GEN_DENSE, RULE_DANTZIG),
+    (4, 61, 80, GEN_DENSE, RULE_DANTZIG),          # ragged blocks (15/15/15/16 rows)
+    (8, 70, 90, GEN_DENSE, RULE_DANTZIG),          # the driver's 8-GPU layout, rehearsed on CPU ranks
+    (8, 41, 41, GEN_DEGENERATE, RULE_BLAND),
 ])
 def test_gloo_row_partition_matches_single_process(world, m, n, kind, rule):
     seed, max_pivots = 12345, 4000

@@ -87,7 +87,8 @@ def lpg():
 
 
 @pytest.mark.parametrize("defer", [None, "0", "5", "64"])
-@pytest.mark.parametrize("world,m,n,kind,rule", [(2, 96, 160, 0, 0), (3, 101, 77, 0, 0), (2, 64, 64, 1, 1)])
+@pytest.mark.parametrize("world,m,n,kind,rule", [(2, 96, 160, 0, 0), (3, 101, 77, 0, 0), (2, 64, 64, 1, 1),
+                                                 (4, 203, 301, 0, 0), (8, 203, 301, 0, 0)])
 def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule, defer, monkeypatch):
     """Row blocks over ranks; default deferred blocks, eager (0), 5- and 64-pivot blocks."""
     if defer is not None:
