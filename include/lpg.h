@@ -107,7 +107,8 @@ typedef struct {
     int32_t world, rank, device;
     int32_t nobj;               /* objective rows (1) */
     int32_t defer_k;            /* pivots per deferred block (0: eager updates) */
-    int32_t pad_;
+    int32_t pivot_wg;           /* workgroups of the persistent pivot kernel (one launch per run of
+                                   pivots, lpg_block.hip); 0: two kernels per pivot */
     double  bytes_per_pivot;    /* algorithmic HBM bytes of one rank-1 update on this rank:
                                    16 * (nrows + nobj) * ncols (one read + one write) */
 } lpg_info_t;

@@ -40,7 +40,7 @@ class Info(ctypes.Structure):
     _fields_ = [("m", ctypes.c_int64), ("ncols", ctypes.c_int64), ("ld", ctypes.c_int64),
                 ("row0", ctypes.c_int64), ("nrows", ctypes.c_int64),
                 ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("nobj", ctypes.c_int32), ("defer_k", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("nobj", ctypes.c_int32), ("defer_k", ctypes.c_int32), ("pivot_wg", ctypes.c_int32),
                 ("bytes_per_pivot", ctypes.c_double)]
 
 

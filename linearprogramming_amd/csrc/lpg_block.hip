@@ -1,0 +1,709 @@
+// lpg_block.hip — the deferred pivot loop as ONE persistent launch per run of
+// pivots (single rank, no communicator): k_pivot_block.
+//
+// What it replaces. Without it every pivot t is two kernels (k_prep_d, then
+// k_select_d, lpg_kernels.hip), and the kernel boundary between them is the
+// grid-wide step where the block partials meet. Each of those kernels then
+// reloads, from the Infinity Cache, the pending-pivot data its chain needs:
+// up to 64 P rows (25 MB at config 3) for the pivot row and 64 C columns
+// (8.4 MB) for the entering column -- at 64 pending pivots that reload, not
+// the arithmetic, is most of the 10-11 us each kernel takes.
+//
+// Here workgroup w (one per CU) owns a fixed slice of the tableau for the
+// whole launch: physical columns [w cw, (w+1) cw) and constraint rows
+// [w rw, (w+1) rw). The slices of the pending P rows and C columns it
+// produces stay in its LDS (sP: KS x cw, sC: KS x rw doubles; 131 KB at
+// config 3), so a chain reads LDS, and only the pivot row's base entries,
+// the entering column's base entries and 64 multipliers per step come from
+// memory. The reference loop this restates is absent upstream
+// (Source/simplex.c:40 -> :65).
+//
+// Per pivot t (pending index q), two phases, each ending in an all-to-all of
+// one record per workgroup ("granules": 16-byte write-through stores whose
+// last word is the pivot's tag, swept by one wave per workgroup until every
+// tag matches -- the data is its own flag, MI355X_MICROARCH.md
+// "allgather" / cdna_hip_programming.md Guideline 16 R2):
+//   P (prep):   ratio records -> leaving row r, pivot element; row r of the
+//               current tableau on this slice's columns = the pending chain
+//               over sP; P_q = row / piv -> sP[q] and Pbuf[q]; the objective
+//               row(s) d = fma(-C_t[obj], P_q, d) (kept in registers for the
+//               launch); the slice's pricing argmin -> pricing record
+//   S (select): pricing records -> entering column k; column k of the
+//               current tableau on this slice's rows = the chain over sC;
+//               column 0 (b) kept current in registers; C_{t+1} -> sC[q+1]
+//               and Cbuf[q+1]; the slice's min-ratio -> ratio record.
+// The arithmetic and every tie-break are k_prep_d / k_select_d's, so the
+// pivot log, the basis and every tableau value are bitwise the same
+// (tests/test_gpu_block.py).
+//
+// Inter-workgroup data: records, P_q entries (read by every slice as the
+// entering column's P_u[k] and P_q[0]) and C_q entries (read as the pivot
+// row's multipliers C_u[r]) are written with sc1 (write-through) stores and
+// read with sc1 loads, after the reading wave saw the record tags that were
+// published behind the writing waves' s_waitcnt vmcnt(0) and a workgroup
+// barrier (MI355X_MICROARCH.md, "Valid forms", first table row). Everything
+// else a workgroup reads was written before the launch. Spins are bounded
+// (~2 s): a workgroup that gives up writes NUMERIC and the flag word
+// DevState::stall, and the launch drains.
+//
+// Residency: one workgroup per CU (the LDS slices force it), as many
+// workgroups as CUs; the launch needs the whole GPU to itself.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "lpg_device.h"
+#include "lpg_internal.h"
+
+namespace lpg {
+
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int kNT = 256;            // threads per workgroup
+constexpr int kMaxWG = 256;         // records swept per phase: 4 per lane of one wave
+constexpr int kPer = kMaxWG / 64;
+constexpr int kRecPMax = 5;         // pricing record granules (k_pivot_block's NGP), space reserved per workgroup
+constexpr int kRecR = 2;            // ratio record:   {theta, key, tag} {piv, row, tag}
+constexpr int kMaxLds = 150 * 1024;   // dynamic LDS cap (the slices)
+constexpr long long kSpinTicks = 200000000ll;   // s_memrealtime runs at 100 MHz: 2 s
+
+// doubles per thread row of the LDS slices: >= ks + 8 (a padded batch),
+// = 2 mod 4 (16-byte reads at this stride from 16 lanes cover the 64 banks)
+__host__ __device__ constexpr int slot_stride(int ks) { return ks + 8 + ((2 - (ks + 8) % 4) + 4) % 4; }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, bytes, 0x00020000);
+}
+// ONE 16-byte write-through store / load (aux 16 = sc1)
+__device__ __forceinline__ void rec_store(__amdgpu_buffer_rsrc_t r, int off, u4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+__device__ __forceinline__ u4 rec_load(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+}
+// 8-byte write-through store / load of a double (global_store/load_dwordx2 sc1)
+__device__ __forceinline__ void st_wt(double *p, double v) {
+    __hip_atomic_store((unsigned long long *)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double *p) {
+    return __longlong_as_double(
+        (long long)__hip_atomic_load((unsigned long long *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ u4 pack(uint64_t a, uint32_t b, uint32_t tag) {
+    return u4{(uint32_t)a, (uint32_t)(a >> 32), b, tag};
+}
+__device__ __forceinline__ uint64_t lo64(const u4 &v) { return ((uint64_t)v.y << 32) | v.x; }
+
+// One wave sweeps the NG-granule records of nwg workgroups until every tag
+// equals `tag`; lane l holds records l, l + 64, l + 128, l + 192. False on
+// timeout (the caller stops the launch).
+template <int NG>
+__device__ bool sweep(__amdgpu_buffer_rsrc_t r, int nwg, uint32_t tag, u4 (&rec)[kPer][NG], int phase,
+                      DevState *st) {
+    const int lane = threadIdx.x & 63;
+    const long long t0 = (long long)wall_clock64();
+    for (;;) {
+        bool ok = true;
+        int bad = -1;
+        uint32_t seen = 0;
+#pragma unroll
+        for (int p = 0; p < kPer; p++) {
+            const int w = lane + 64 * p;
+            if (w < nwg) {
+#pragma unroll
+                for (int k = 0; k < NG; k++) rec[p][k] = rec_load(r, (w * NG + k) * 16);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < kPer; p++) {
+            const int w = lane + 64 * p;
+            if (w < nwg) {
+#pragma unroll
+                for (int k = 0; k < NG; k++)
+                    if (rec[p][k].w != tag) {
+                        ok = false;
+                        if (bad < 0) {
+                            bad = w * NG + k;
+                            seen = rec[p][k].w;
+                        }
+                    }
+            }
+        }
+        if (__all(ok)) return true;
+        if ((long long)wall_clock64() - t0 > kSpinTicks) {
+            const int wl = winner_lane(!ok);
+            const int bi = (int)rdl32((uint32_t)bad, wl);
+            const uint32_t sv = rdl32(seen, wl);
+            if (lane == 0) {
+                st->stall_info[0] = phase;
+                st->stall_info[1] = tag;
+                st->stall_info[2] = bi;
+                st->stall_info[3] = sv;
+            }
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// lexicographic min over this lane's records, then over the wave; src = the
+// winner's workgroup (uniform), -1 if every key is (~0, ~0); pay[k] = its
+// granule k + 1 (uniform)
+template <int NG>
+__device__ __forceinline__ void rec_min(const u4 (&rec)[kPer][NG], int nwg, uint64_t &h, uint32_t &l, int &src,
+                                        u4 (&pay)[NG > 1 ? NG - 1 : 1]) {
+    const int lane = threadIdx.x & 63;
+    h = ~0ull;
+    l = ~0u;
+    int mine = -1;
+    u4 mp[NG > 1 ? NG - 1 : 1];
+#pragma unroll
+    for (int k = 0; k + 1 < NG; k++) mp[k] = u4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int p = 0; p < kPer; p++) {
+        const int w = lane + 64 * p;
+        if (w < nwg) {
+            const uint64_t a = lo64(rec[p][0]);
+            const uint32_t b = rec[p][0].z;
+            if (key_less(a, b, h, l)) {
+                h = a;
+                l = b;
+                mine = w;
+#pragma unroll
+                for (int k = 0; k + 1 < NG; k++) mp[k] = rec[p][k + 1];
+            }
+        }
+    }
+    const uint64_t mh = h;
+    const uint32_t ml = l;
+    wave_min_key(h, l);
+    const int wl = winner_lane(mine >= 0 && mh == h && ml == l);
+    src = (wl < 0 || (h == ~0ull && l == ~0u)) ? -1 : (int)rdl32((uint32_t)mine, wl);
+#pragma unroll
+    for (int k = 0; k + 1 < NG; k++)
+        pay[k] = wl < 0 ? u4{0u, 0u, 0u, 0u}
+                        : u4{rdl32(mp[k].x, wl), rdl32(mp[k].y, wl), rdl32(mp[k].z, wl), rdl32(mp[k].w, wl)};
+}
+
+struct Bcast {            // one phase's decision, from wave 0 to the workgroup
+    uint64_t h;
+    uint32_t l;
+    int32_t ok;           // 1: decided, 0: none (OPTIMAL / UNBOUNDED), -1: timeout
+    uint64_t p0, p1, p2, p3;   // winner payload
+    uint64_t z;           // P_q[0]
+};
+
+}  // namespace
+
+#ifdef LPG_PHASES
+// Phase probe (tools/block_probe.py; tools/liblpg_phases.so only): s_memrealtime
+// stamps of thread 0 of workgroups 0 and nwg / 2 at the phase boundaries of
+// every pivot of the launch.
+__device__ unsigned long long g_bph[2][64][8];
+#define LPG_BPH(t, k)                                                                          \
+    do {                                                                                       \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                            \
+        if (tid == 0 && (wg == 0 || wg == nwg / 2) && (t) < 64)                                \
+            g_bph[wg == 0 ? 0 : 1][(t)][(k)] = __builtin_amdgcn_s_memrealtime();               \
+    } while (0)
+int debug_block_phases(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bph), sizeof g_bph) == hipSuccess ? 0 : -1;
+}
+#else
+#define LPG_BPH(t, k) do { } while (0)
+#endif
+
+struct BlockArgs {
+    double *T;
+    Geo g;
+    DevState *st;
+    int s0, q0, n;               // parity and pending index of the first pivot; pivots in this launch
+    Cand *part;                  // in: ncand ratio candidates; out: one per workgroup, none up to ncand
+    int ncand;
+    const double *Cs0;           // C[s0]: the first pivot's column snapshot (incl. objective rows)
+    double *Cs1;                 // C[(s0 + n) & 1]: the snapshot the launch leaves behind
+    Defer D;
+    u4 *rec;                     // nwg * (kRecPMax + kRecR) granules
+    uint32_t tag0;               // tag of pivot i of this launch = tag0 + 1 + i (never repeats per context)
+    int nwg, cw, rw, ks;         // workgroups, columns / rows per slice, LDS slots
+};
+
+template <int RULE, int NOBJ>
+__global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
+    // pricing record granules: {key, j} {dR, phys} {P_q[phys]} {P_q[0] (workgroup 0)} [{dM}]
+    constexpr int NGP = NOBJ == 2 ? 5 : 4;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ Bcast bc;
+    // per wave, by pending slot: the pivot row's multipliers -C_u[r] (phase P)
+    // and the entering column's P_u[k] (phase S); slots 64..71 are the
+    // padding a batch of 8 may reach: -0 and +0, so a padded step
+    // fma(-0, +0, x) / fma(-(+0), +0, x) is exactly x
+    __shared__ __attribute__((aligned(16))) double wm[kNT / 64][72], wp[kNT / 64][72];
+    const Geo &g = a.g;
+    const Defer &D = a.D;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wg = blockIdx.x, nwg = a.nwg, cw = a.cw, rw = a.rw, ks = a.ks;
+    // thread-major slices: sP[col][slot], sC[row][slot], a row of S = slot_stride(ks)
+    // doubles (>= ks + 8, = 2 mod 4: 16-byte reads of 16 consecutive lanes hit all
+    // 64 banks once). Slots past the pending block stay +0, so the chains'
+    // padding steps (a batch of 8 past q) are exact no-ops.
+    const int S = slot_stride(ks);
+    double *sP = lds;
+    double *sC = lds + (size_t)S * cw;
+    double *sPt = sP + (size_t)(tid < cw ? tid : cw - 1) * S;   // this thread's slots (clamped: in bounds)
+    double *sCt = sC + (size_t)(tid < rw ? tid : rw - 1) * S;
+    const int64_t ncp = (g.ncols + 1) & ~(int64_t)1;   // columns incl. the even padding one (k_flushw reads pairs)
+    const int64_t c = (int64_t)wg * cw + tid;          // this thread's physical column
+    const bool hc = tid < cw && c < ncp;
+    const int64_t i = (int64_t)wg * rw + tid;          // this thread's local constraint row
+    const bool hr = tid < rw && i < g.nloc;
+    const int64_t rM = g.nloc, rR = g.nloc + NOBJ - 1;
+    const __amdgpu_buffer_rsrc_t recP = rsrc(a.rec, nwg * NGP * 16);
+    const __amdgpu_buffer_rsrc_t recR = rsrc(a.rec + nwg * kRecPMax, nwg * kRecR * 16);
+    DevState *st = a.st;
+
+    // ---- launch start: everything here was written before the launch
+    int s = a.s0;
+    const int32_t status0 = st->slot[s].status;
+    int64_t kt = st->slot[s].k;                        // entering column (logical) of the first pivot
+    double cobjM = NOBJ == 2 ? a.Cs0[rM] : 0.0, cobjR = a.Cs0[rR];
+    double dM = 0.0, dR = 0.0;
+    int32_t lj = 0;
+    if (hc) {
+        if (NOBJ == 2) dM = g.T[rM * g.ld + c];
+        dR = g.T[rR * g.ld + c];
+        lj = D.colmap[c];
+    }
+    int64_t rqv = lane < a.q0 ? D.rq[lane] : -1;       // lane u: r_u of pending pivot u
+    for (int u = 0; u < S; u++) {
+        if (tid < cw) sPt[u] = (u < a.q0 && hc) ? D.Pbuf[(int64_t)u * g.ld + c] : 0.0;
+        if (tid < rw) sCt[u] = (u < a.q0 && hr) ? D.Cbuf[(int64_t)u * D.cs + i] : 0.0;
+    }
+    double b = 0.0;                                    // column 0 of the current tableau, this thread's row
+    int64_t mybasis = 0;
+    int lastpiv = -1;                                  // last pending pivot on this thread's row
+    if (hr) {
+        const double cq = a.Cs0[i];
+        sCt[a.q0] = cq;
+        st_wt(D.Cbuf + (int64_t)a.q0 * D.cs + i, cq);   // read as a multiplier by other slices later
+        b = g.T[i * g.ld];
+        mybasis = D.basis[g.row0 + i];
+    }
+    {
+        const double p0l = lane < a.q0 ? D.Pbuf[(int64_t)lane * g.ld] : 0.0;
+        const uint64_t p0b = (uint64_t)__double_as_longlong(p0l);
+        for (int u = 0; u < a.q0; u++) {               // b = the pending chain over the earlier pivots
+            const double p0 = __longlong_as_double((long long)rdl64(p0b, u));
+            const int64_t ru = (int64_t)rdl64((uint64_t)rqv, u);
+            if (hr) {
+                b = (i == ru) ? p0 : fma(-sCt[u], p0, b);
+                if (i == ru) lastpiv = u;
+            }
+        }
+    }
+    if (lane < 8) {
+        wm[wave][64 + lane] = -0.0;
+        wp[wave][64 + lane] = 0.0;
+    }
+    __syncthreads();
+    bool stop = status0 != RUNNING;
+    if (stop && wg == 0 && tid == 0) st->slot[s ^ 1].status = status0;
+    double p0q = 0.0;                                  // P_q[0] of the current pivot (workgroup 0's record)
+
+    for (int t = 0; t < a.n && !stop; t++) {
+        const int q = a.q0 + t;
+        const uint32_t tag = a.tag0 + 1 + (uint32_t)t;
+        LPG_BPH(t, 0);
+        // ================= phase P: the leaving row and the pivot row
+        if (wave == 0) {
+            uint64_t h = ~0ull, p0 = 0, p1 = 0;
+            uint32_t l = ~0u;
+            int src = -1;
+            bool ok = true;
+            if (t == 0) {
+                // candidates of the previous select (k_select_d, a bootstrap or the previous launch)
+                uint64_t mh = ~0ull, mp0 = 0, mp1 = 0;
+                uint32_t ml = ~0u;
+                for (int e = lane; e < a.ncand; e += 64) {
+                    const Cand cd = a.part[e];
+                    if (cd.row < 0) continue;
+                    const uint64_t ch = (uint64_t)__double_as_longlong(cd.theta);
+                    const uint32_t cl = (uint32_t)cd.key;
+                    if (key_less(ch, cl, mh, ml)) {
+                        mh = ch;
+                        ml = cl;
+                        mp0 = (uint64_t)__double_as_longlong(cd.piv);
+                        mp1 = (uint64_t)cd.row;
+                    }
+                }
+                h = mh;
+                l = ml;
+                wave_min_key(h, l);
+                const int wl = winner_lane(mh == h && ml == l && mh != ~0ull);
+                if (wl >= 0 && !(h == ~0ull && l == ~0u)) {
+                    src = 0;
+                    p0 = rdl64(mp0, wl);
+                    p1 = rdl64(mp1, wl);
+                }
+            } else {
+                u4 rec[kPer][kRecR], pay[kRecR - 1];
+                ok = sweep<kRecR>(recR, nwg, tag - 1, rec, 1, st);
+                if (ok) {
+                    rec_min<kRecR>(rec, nwg, h, l, src, pay);
+                    p0 = lo64(pay[0]);          // pivot element
+                    p1 = pay[0].z;              // leaving row
+                }
+            }
+            if (lane == 0) {
+                bc.h = h;
+                bc.l = l;
+                bc.ok = !ok ? -1 : (src >= 0 ? 1 : 0);
+                bc.p0 = p0;
+                bc.p1 = p1;
+            }
+        }
+        __syncthreads();
+        LPG_BPH(t, 1);
+        const int okP = bc.ok;
+        const double theta = __longlong_as_double((long long)bc.h);
+        const double piv = __longlong_as_double((long long)bc.p0);
+        const int64_t r = (int64_t)bc.p1;               // leaving row (local == global: one rank)
+        __syncthreads();                                // bc is rewritten by the next phase
+        if (okP <= 0 || !isfinite(piv) || !isfinite(theta)) {
+            if (wg == 0 && tid == 0) {
+                const int32_t sv = okP < 0 ? NUMERIC : (okP == 0 ? UNBOUNDED : NUMERIC);
+                st->slot[s].status = sv;
+                st->slot[s].r = -1;
+                st->slot[s ^ 1].status = sv;
+                if (okP < 0) st->stall = 1;
+            }
+            break;
+        }
+        if (wg == 0 && tid == 0) {                      // k_prep_d's bookkeeping
+            st->slot[s].r = r;
+            D.rq[q] = r;
+            st->npend = q + 1;
+            D.kq[q] = kt;
+            D.lv[q] = D.basis[r];
+            D.pv[q] = piv;
+            D.basis[r] = kt;
+            const int64_t np = st->pivots;
+            if (D.logk && np < st->logcap) {
+                D.logk[np] = kt;
+                D.logr[np] = r;
+            }
+            st->pivots = np + 1;
+            st->last_k = kt;
+            st->last_r = r;
+        }
+        if (hr && i == r) {
+            mybasis = kt;
+            lastpiv = q;
+        }
+        // multipliers -C_u[r] (lane u < q; -0 past q), the pivot row's restart point
+        wm[wave][lane] = lane < q ? -ld_wt(D.Cbuf + (int64_t)lane * D.cs + r) : -0.0;
+        const unsigned long long hit = __ballot(lane < q && rqv == r);
+        const int qs = hit ? 63 - __clzll((long long)hit) : -1;
+        if (lane == q) rqv = r;
+        double x = hc ? g.T[r * g.ld + c] : 0.0;
+        LPG_BPH(t, 2);
+        int u = 0;
+        if (qs >= 0) {
+            x = sPt[qs];
+            u = qs + 1;
+        }
+        if ((u & 1) && u < q) {                         // one step to reach an even slot (16-byte reads)
+            x = fma(wm[wave][u], sPt[u], x);
+            u++;
+        }
+        // the pending chain in batches of 8 (slots past q are (P = +0,
+        // multiplier = -0): exact no-ops), the next batch's LDS reads issued
+        // before this batch's fmas
+        if (u < q) {
+            d2 pv[4], mv[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                pv[j] = *(const d2 *)(sPt + u + 2 * j);
+                mv[j] = *(const d2 *)(&wm[wave][u + 2 * j]);
+            }
+            for (;;) {
+                const bool more = u + 8 < q;
+                d2 pn[4], mn[4];
+                if (more) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        pn[j] = *(const d2 *)(sPt + u + 8 + 2 * j);
+                        mn[j] = *(const d2 *)(&wm[wave][u + 8 + 2 * j]);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    x = fma(mv[j].x, pv[j].x, x);
+                    x = fma(mv[j].y, pv[j].y, x);
+                }
+                if (!more) break;
+                u += 8;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    pv[j] = pn[j];
+                    mv[j] = mn[j];
+                }
+            }
+        }
+        drain();                                        // the previous phase's C stores, before this record
+        PricePart pb{0.0, -1, 0, 0};
+        double pq = 0.0;
+        if (hc) {
+            pq = x / piv;
+            sPt[q] = pq;
+            st_wt(D.Pbuf + (int64_t)q * g.ld + c, pq);  // drained in phase S, before the ratio record
+            if (NOBJ == 2) dM = fma(-cobjM, pq, dM);
+            dR = fma(-cobjR, pq, dR);
+            price_one<RULE>(pb, dM, dR, lj, g, c);
+            pb.pad = (int32_t)c;
+        }
+        pb = block_argmin_pp<RULE, kNT / 64>(pb);
+        if (tid == 0) {
+            uint64_t h = ~0ull;
+            uint32_t l = ~0u;
+            if (pb.j >= 0) {
+                h = RULE == RULE_BLAND ? 0ull
+                                       : (((uint64_t)(uint32_t)pb.cls << 63) |
+                                          (~(uint64_t)__double_as_longlong(pb.v) & 0x7fffffffffffffffull));
+                l = (uint32_t)pb.j;
+            }
+            rec_store(recP, (wg * NGP + 0) * 16, pack(h, l, tag));
+            // P_q[0] for every slice's column 0 (workgroup 0 holds column 0 in thread 0)
+            rec_store(recP, (wg * NGP + 3) * 16, pack((uint64_t)__double_as_longlong(wg == 0 ? pq : 0.0), 0u, tag));
+        }
+        // the slice winner's objective entries and P_q entry ride along (C_{t+1}[obj]
+        // and P_q[k] if it wins the grid); the thread of that column holds them
+        if (pb.j >= 0 && hc && (int64_t)lj == pb.j) {
+            rec_store(recP, (wg * NGP + 1) * 16, pack((uint64_t)__double_as_longlong(dR), (uint32_t)c, tag));
+            rec_store(recP, (wg * NGP + 2) * 16, pack((uint64_t)__double_as_longlong(pq), 0u, tag));
+            if (NOBJ == 2) rec_store(recP, (wg * NGP + 4) * 16, pack((uint64_t)__double_as_longlong(dM), 0u, tag));
+        }
+        if (pb.j < 0 && tid == 0) {
+            rec_store(recP, (wg * NGP + 1) * 16, pack(0ull, 0u, tag));
+            rec_store(recP, (wg * NGP + 2) * 16, pack(0ull, 0u, tag));
+            if (NOBJ == 2) rec_store(recP, (wg * NGP + 4) * 16, pack(0ull, 0u, tag));
+        }
+        LPG_BPH(t, 3);
+
+        // ================= phase S: the entering column and the ratio test
+        if (wave == 0) {
+            u4 rec[kPer][NGP], pay[NGP - 1];
+            const bool ok = sweep<NGP>(recP, nwg, tag, rec, 2, st);
+            uint64_t h = ~0ull, p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+            uint32_t l = ~0u;
+            int src = -1;
+            if (ok) {
+                rec_min<NGP>(rec, nwg, h, l, src, pay);
+                p0 = lo64(pay[0]);              // dR at the entering column
+                p1 = pay[0].z;                  // its physical column
+                p2 = lo64(pay[1]);              // P_q at the entering column
+                if (NOBJ == 2) p3 = lo64(pay[NGP - 2]);   // dM
+                // P_q[0]: workgroup 0's record, held by lane 0
+                if (lane == 0) bc.z = lo64(rec[0][3]);
+            }
+            if (lane == 0) {
+                bc.h = h;
+                bc.l = l;
+                bc.ok = !ok ? -1 : (src >= 0 ? 1 : 0);
+                bc.p0 = p0;
+                bc.p1 = p1;
+                bc.p2 = p2;
+                bc.p3 = p3;
+            }
+        }
+        __syncthreads();
+        LPG_BPH(t, 4);
+        const int okS = bc.ok;
+        const int64_t kn = (int64_t)bc.l;               // logical entering column of pivot t + 1
+        const int64_t kp = (int64_t)bc.p1;              // its physical column
+        const double nR = __longlong_as_double((long long)bc.p0), nM = __longlong_as_double((long long)bc.p3);
+        const double pkq = __longlong_as_double((long long)bc.p2);
+        p0q = __longlong_as_double((long long)bc.z);
+        __syncthreads();
+        const int s1 = s ^ 1;
+        if (okS <= 0) {
+            if (wg == 0 && tid == 0) {
+                const int32_t sv = okS < 0 ? NUMERIC : OPTIMAL;
+                st->slot[s1].status = sv;
+                st->slot[s1].k = -1;
+                st->slot[s1].r = -1;
+                st->slot[s].status = sv;
+                if (okS < 0) st->stall = 1;
+            }
+            break;
+        }
+        if (wg == 0 && tid == 0) {
+            st->slot[s1].status = RUNNING;
+            st->slot[s1].k = kn;
+        }
+        // column k of the current tableau; P_u[k] (lane u < q from Pbuf, P_q[k]
+        // from the record; +0 past q)
+        double xa = hr ? g.T[i * g.ld + kp] : 0.0;
+        if (wave * 64 < rw)                             // waves holding rows
+            wp[wave][lane] = lane < q ? ld_wt(D.Pbuf + (int64_t)lane * g.ld + kp) : (lane == q ? pkq : 0.0);
+        LPG_BPH(t, 6);
+        if (hr) b = (i == r) ? p0q : fma(-sCt[q], p0q, b);
+        // the chain in batches of 8 (slots past q are (C = +0, P = +0): exact
+        // no-ops). A row pivoted earlier in this block restarts at its last
+        // pivot lp: x = P_lp[k], and the steps up to lp become (+0, +0) no-ops
+        // (operand selects, off the dependent fma chain).
+        if (hr && lastpiv >= 0) xa = wp[wave][lastpiv];
+        {
+            d2 cv[4], pk[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                cv[j] = *(const d2 *)(sCt + 2 * j);
+                pk[j] = *(const d2 *)(&wp[wave][2 * j]);
+            }
+            for (int v = 0;; v += 8) {
+                const bool more = v + 8 <= q;
+                d2 cn[4], pn[4];
+                if (more) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        cn[j] = *(const d2 *)(sCt + v + 8 + 2 * j);
+                        pn[j] = *(const d2 *)(&wp[wave][v + 8 + 2 * j]);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const bool l0 = v + 2 * j > lastpiv, l1 = v + 2 * j + 1 > lastpiv;
+                    xa = fma(-(l0 ? cv[j].x : 0.0), l0 ? pk[j].x : 0.0, xa);
+                    xa = fma(-(l1 ? cv[j].y : 0.0), l1 ? pk[j].y : 0.0, xa);
+                }
+                if (!more) break;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    cv[j] = cn[j];
+                    pk[j] = pn[j];
+                }
+            }
+        }
+        LPG_BPH(t, 7);
+        drain();                                        // this pivot's P stores, before the ratio record
+        const bool last = t + 1 == a.n;
+        Cand cd{0.0, 0.0, 0, -1};
+        if (hr) {
+            if (!last) {
+                sCt[q + 1] = xa;
+                st_wt(D.Cbuf + (int64_t)(q + 1) * D.cs + i, xa);   // drained in the next phase P
+            } else {
+                a.Cs1[i] = xa;
+            }
+            if (xa > g.eps_piv) {
+                cd.theta = b > 0.0 ? b / xa : 0.0;
+                cd.piv = xa;
+                cd.row = g.row0 + i;
+                cd.key = RULE == RULE_BLAND ? mybasis : g.row0 + i;
+            }
+        }
+        cd = block_argmin_cand<kNT / 64>(cd);
+        if (tid == 0) {
+            uint64_t h = ~0ull;
+            uint32_t l = ~0u;
+            if (cd.row >= 0) {
+                h = (uint64_t)__double_as_longlong(cd.theta);
+                l = (uint32_t)cd.key;
+            }
+            rec_store(recR, (wg * kRecR + 0) * 16, pack(h, l, tag));
+            rec_store(recR, (wg * kRecR + 1) * 16,
+                      pack((uint64_t)__double_as_longlong(cd.piv), (uint32_t)cd.row, tag));
+            if (last) a.part[wg] = cd;
+        }
+        if (last && wg == 0 && tid == 0) {
+            a.Cs1[rR] = nR;
+            if (NOBJ == 2) a.Cs1[rM] = nM;
+            for (int e = nwg; e < a.ncand; e++) a.part[e] = Cand{0.0, 0.0, -1, -1};
+        }
+        LPG_BPH(t, 5);
+        kt = kn;
+        cobjR = nR;
+        cobjM = nM;
+        s = s1;
+    }
+    // the objective row(s) of this slice, current after the last applied pivot
+    if (hc) {
+        if (NOBJ == 2) g.T[rM * g.ld + c] = dM;
+        g.T[rR * g.ld + c] = dR;
+    }
+}
+
+// ---- host side -------------------------------------------------------------
+
+int block_records_bytes(int nwg) { return nwg * (kRecPMax + kRecR) * 16; }
+
+int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, int *rw, size_t *lds) {
+    const int64_t ncp = (g.ncols + 1) & ~(int64_t)1;
+    int w = want > 0 ? want : cus;
+    if (w > kMaxWG) w = kMaxWG;
+    if (w > cus) w = cus;
+    if (w < 1) return -1;
+    const int64_t c = (ncp + w - 1) / w, r = (g.nloc + w - 1) / w;
+    if (c > kNT || r > kNT) return -1;
+    const size_t bytes = (size_t)slot_stride(ks) * (size_t)(c + r) * sizeof(double);
+    if (bytes > (size_t)kMaxLds) return -1;
+    *nwg = w;
+    *cw = (int)c;
+    *rw = (int)r;
+    *lds = bytes;
+    return 0;
+}
+
+int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, int s0, int q0, int n, Cand *part,
+                       int ncand, const double *Cs0, double *Cs1, const Defer &D, void *rec, uint32_t tag0, int nwg,
+                       int cw, int rw, int ks, size_t lds) {
+    if (n < 1 || q0 < 0 || q0 + n > ks || ks > 64 || nwg < 1 || nwg > kMaxWG || ncand < nwg) return -1;
+    if ((int64_t)nwg * cw < ((g.ncols + 1) & ~(int64_t)1) || (int64_t)nwg * rw < g.nloc) return -1;
+    if (g.nobj != 1 && g.nobj != 2) return -1;
+    BlockArgs a;
+    a.T = g.T;
+    a.g = g;
+    a.st = st;
+    a.s0 = s0;
+    a.q0 = q0;
+    a.n = n;
+    a.part = part;
+    a.ncand = ncand;
+    a.Cs0 = Cs0;
+    a.Cs1 = Cs1;
+    a.D = D;
+    a.rec = (u4 *)rec;
+    a.tag0 = tag0;
+    a.nwg = nwg;
+    a.cw = cw;
+    a.rw = rw;
+    a.ks = ks;
+    hipStream_t stream = (hipStream_t)L.stream;
+#define LPG_PB(R, NO)                                                                                   \
+    do {                                                                                                \
+        static bool attr = false;                                                                       \
+        if (!attr) {                                                                                    \
+            if (hipFuncSetAttribute((const void *)k_pivot_block<R, NO>,                                 \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds) != hipSuccess) \
+                return -1;                                                                              \
+            attr = true;                                                                                \
+        }                                                                                               \
+        hipLaunchKernelGGL((k_pivot_block<R, NO>), dim3(nwg), dim3(kNT), lds, stream, a);              \
+    } while (0)
+    if (rule == RULE_BLAND) {
+        if (g.nobj == 2) LPG_PB(RULE_BLAND, 2);
+        else LPG_PB(RULE_BLAND, 1);
+    } else {
+        if (g.nobj == 2) LPG_PB(RULE_DANTZIG, 2);
+        else LPG_PB(RULE_DANTZIG, 1);
+    }
+#undef LPG_PB
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace lpg

@@ -61,6 +61,13 @@ struct lpg_ctx {
     int npp = 0, nsel = 0;
     int npp_d = 0, nsel_d = 0;    // the same partial counts for the single-rank deferred pair (k_prep_d / k_select_d)
     int pivot_nt = kPivotThreads; // threads per block of that pair
+    // the persistent block kernel (lpg_block.hip): single rank, deferred, the
+    // default where its slices fit (LPG_PERSIST=0 turns it off)
+    bool persist = false;
+    int pb_nwg = 0, pb_cw = 0, pb_rw = 0;
+    size_t pb_lds = 0;
+    void *rec = nullptr;          // its records (zeroed once; tags never repeat within a context)
+    uint32_t tag = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
     // pivot-loop host state
@@ -408,6 +415,34 @@ static constexpr int kDefaultDeferSmall = 32;   // tableaus below 512 MB per ran
 
 static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule);
 
+// Ratio candidates in `part` that a consumer reads: every producer writes
+// its own count and the bootstraps clear the rest (clear_candidates).
+static int cand_cap(const lpg_ctx *c) { return std::max(c->nsel, c->nsel_d); }
+
+// Persistent path: one k_pivot_block launch per run of pivots inside a
+// block, the block's flush after its last pivot.
+static int enqueue_blocks(lpg_ctx *c, int64_t npiv, int rule) {
+    const Geo g = geo(c);
+    while (npiv > 0) {
+        const int n = (int)std::min<int64_t>(npiv, c->defer_k - c->pend);
+        const int s0 = c->par, s1 = (s0 + n) & 1;
+        if (launch_pivot_block(lau(c), g, rule, c->st, s0, c->pend, n, c->part, cand_cap(c), c->C[s0], c->C[s1],
+                               defer_of(c, c->pend), c->rec, c->tag, c->pb_nwg, c->pb_cw, c->pb_rw, c->defer_k,
+                               c->pb_lds))
+            return fail(c, LPG_ERR_DEVICE, "pivot block launch failed");
+        c->tag += (uint32_t)n;
+        c->pend += n;
+        c->par = s1;
+        c->enq += n;
+        npiv -= n;
+        if (c->pend == c->defer_k) {
+            int rc = flush_launch(c);
+            if (rc) return rc;
+        }
+    }
+    return 0;
+}
+
 static void graph_drop(lpg_ctx *c) {
     for (int p = 0; p < 2; p++) {
         if (c->graph[p]) (void)hipGraphExecDestroy(c->graph[p]);
@@ -457,6 +492,7 @@ static int enqueue(lpg_ctx *c, int64_t npiv, int rule) {
         int rc = bootstrap(c, rule);
         if (rc) return rc;
     }
+    if (c->persist && !has_comm(c)) return enqueue_blocks(c, npiv, rule);
     const int G = graph_len(c);
     // eager-mode timing brackets every update, which a graph cannot; deferred
     // timing brackets only the flushes, which stay outside the graph
@@ -562,6 +598,12 @@ static int read_result(lpg_ctx *c, lpg_result *out, int rule) {
     double z = 0;
     HIPCHK(c, hipMemcpyAsync(&z, c->T + (c->nloc + c->nobj - 1) * c->ld, sizeof z, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (h.stall)
+        return fail(c, LPG_ERR_DEVICE,
+                    "k_pivot_block: a workgroup waited > 2 s for the others (phase %lld, tag %lld, record %lld "
+                    "showed tag %lld; is another kernel holding CUs? LPG_PERSIST=0 uses the two-kernel pivot)",
+                    (long long)h.stall_info[0], (long long)h.stall_info[1], (long long)h.stall_info[2],
+                    (long long)h.stall_info[3]);
     if (out) {
         const int32_t s = c->booted ? h.slot[c->par].status : RUNNING;
         out->status = s == RUNNING ? LPG_ITER_LIMIT : s;
@@ -691,6 +733,16 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     // k_select_d: one row per thread; with world > 1 the count must be the
     // same on every rank (the candidates are allgathered)
     c->nsel_d = world == 1 ? pivot_d_blocks(g, 1, c->pivot_nt) : (int)((maxloc + 255) / 256);
+    {
+        const char *pe = getenv("LPG_PERSIST"), *pw = getenv("LPG_PERSIST_WG");
+        int cus = 0;
+        if (world == 1 && c->defer_k > 0 && c->fast_pivot && !(pe && atoi(pe) == 0) &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+            block_geometry(g, c->defer_k, cus, pw ? atoi(pw) : 0, &c->pb_nwg, &c->pb_cw, &c->pb_rw, &c->pb_lds) == 0) {
+            c->persist = true;
+            c->nsel_d = c->pb_nwg;          // one ratio candidate per workgroup
+        }
+    }
 #define ALLOC(p, bytes)                                                                    \
     do {                                                                                   \
         hipError_t e_ = hipMalloc((void **)&(p), (bytes));                                 \
@@ -711,6 +763,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     ALLOC(c->pp, (size_t)std::max(c->npp, c->npp_d) * sizeof(PricePart));
     ALLOC(c->pc, (size_t)c->npp * sizeof(int));
     ALLOC(c->part, (size_t)std::max(c->nsel, c->nsel_d) * sizeof(Cand));
+    if (c->persist) ALLOC(c->rec, (size_t)block_records_bytes(c->pb_nwg));
     if (world > 1) ALLOC(c->cand, (size_t)std::max(c->nsel, c->nsel_d) * world * sizeof(Cand));
     else c->cand = c->part;
     ALLOC(c->basis, (size_t)m * sizeof(int64_t));
@@ -744,6 +797,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         hipMemset(c->basis, 0, (size_t)m * sizeof(int64_t)) != hipSuccess ||
         (c->Cbuf && hipMemset(c->Cbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->cs * sizeof(double)) != hipSuccess) ||
         (c->zrow && hipMemset(c->zrow, 0, (size_t)c->ld * sizeof(double)) != hipSuccess) ||
+        (c->rec && hipMemset(c->rec, 0, (size_t)block_records_bytes(c->pb_nwg)) != hipSuccess) ||
         (c->colmap && (launch_iota(lau(c), c->colmap, c->ld) || launch_iota(lau(c), c->inv, c->ld)))) {
         fail(c, LPG_ERR_DEVICE, "hipMemset failed");
         lpg_destroy(c);
@@ -775,6 +829,11 @@ int lpg_comm_unique_id(void *uid, size_t len) {
 // With a communicator the deferred pair runs in 256-thread blocks (its
 // candidate count must match across ranks): drop a 128-thread choice.
 static void comm_pivot_blocks(lpg_ctx *c) {
+    if (c->persist) {                                  // the persistent kernel is single-rank only
+        c->persist = false;
+        c->nsel_d = pivot_d_blocks(geo(c), 1, 256);    // <= the allocation (sized for max(nsel, nwg))
+        c->booted = false;
+    }
     if (c->pivot_nt == 256) return;
     c->pivot_nt = 256;
     c->npp_d = pivot_d_blocks(geo(c), 0, 256);    // buffers were sized for the larger 128-thread counts
@@ -821,7 +880,8 @@ void lpg_destroy(lpg_ctx *c) {
     for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
-                    c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->mul, c->pv, c->tmp};
+                    c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->mul, c->pv, c->tmp,
+                    c->rec};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -840,7 +900,7 @@ int lpg_info(const lpg_ctx *c, lpg_info_t *o) {
     o->device = c->device;
     o->nobj = (int32_t)c->nobj;
     o->defer_k = c->defer_k;
-    o->pad_ = 0;
+    o->pivot_wg = c->persist ? c->pb_nwg : 0;
     o->bytes_per_pivot = 16.0 * (double)(c->nloc + c->nobj) * (double)c->ncols;
     return 0;
 }
@@ -979,6 +1039,7 @@ int lpg_prepare(lpg_ctx *c, int rule) {
     if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
     if (!c->booted || c->boot_rule != rule)
         if ((rc = bootstrap(c, rule))) return rc;
+    if (c->persist && !has_comm(c)) return 0;   // one launch per block: nothing to capture
     // the conditions under which enqueue replays graphs (enqueue, above)
     const int G = graph_len(c);
     const bool timed = c->timing && c->defer_k == 0;
@@ -1297,6 +1358,7 @@ int lpg_device_sync(lpg_ctx *c) {
 #ifdef LPG_PHASES
 // tools/phase_probe.py only (not part of include/lpg.h; absent from liblpg.so)
 int lpg_debug_phases(unsigned long long *out, int reset) { return lpg::debug_phases(out, reset); }
+int lpg_debug_block_phases(unsigned long long *out) { return lpg::debug_block_phases(out); }
 #endif
 
 }  // extern "C"

@@ -51,6 +51,8 @@ struct DevState {
     unsigned long long work[2];   // k_update work-item dequeue heads, per pivot parity (reset by k_prep)
     int64_t npend;                // deferred pivots applied but not yet flushed (prep_t sets q + 1)
     unsigned long long fwork;     // k_flush work-item dequeue head (reset with npend after each flush)
+    int64_t stall;                // set by k_pivot_block when a workgroup gave up waiting (lpg_block.hip)
+    int64_t stall_info[4];        // its view then: phase (1 P, 2 S), expected tag, record index, tag seen
 };
 
 // Pending-pivot buffers of the deferred update (Defer::on == 0: eager mode).
@@ -137,6 +139,17 @@ int launch_prep_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s,
 int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, const double *Cs,
                      double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part, int nsel,
                      const Defer &D);
+// The deferred pivot loop as one persistent launch of n pivots starting at
+// pending index q0 (lpg_block.hip): nwg workgroups, one per CU, each owning
+// cw physical columns and rw constraint rows, with ks pending slots of their
+// P / C slices in lds bytes of LDS. block_geometry picks the split (-1: the
+// slices do not fit, use k_prep_d / k_select_d); the records buffer holds
+// block_records_bytes(nwg) zero-initialised bytes; tags start after tag0.
+int block_records_bytes(int nwg);
+int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, int *rw, size_t *lds);
+int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, int s0, int q0, int n, Cand *part,
+                       int ncand, const double *Cs0, double *Cs1, const Defer &D, void *rec, uint32_t tag0, int nwg,
+                       int cw, int rw, int ks, size_t lds);
 // Apply the pending pivots (st->npend <= kmax) to constraint rows 0..nloc-1.
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which);
 // ... in two parts: the block pass itself (k_flushw / k_flushm / k_flush), then
@@ -173,6 +186,7 @@ int launch_dual_pivot(const Launch &L, const Geo &g, DevState *st, int s, Cand *
 
 #ifdef LPG_PHASES
 int debug_phases(unsigned long long *out, int reset);   // tools/phase_probe.py
+int debug_block_phases(unsigned long long *out);        // tools/block_probe.py
 #endif
 int price_blocks(const Geo &g);      // number of pricing partials (= prep / price grid)
 int update_variants();               // entries of the update-kernel variant table

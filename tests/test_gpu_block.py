@@ -1,0 +1,174 @@
+"""The persistent pivot kernel (k_pivot_block, lpg_block.hip) vs the oracle
+and vs the two-kernel pivot (k_prep_d / k_select_d), bitwise.
+
+One launch runs a whole run of pivots: each workgroup keeps its slice of the
+pending P rows and C columns in LDS, and the per-pivot grid decisions are
+all-to-alls of write-through records inside the launch. The arithmetic and
+the tie-breaks are the two-kernel pair's, so pivot logs, bases and whole
+tableaus must equal the oracle's (np.array_equal) for every workgroup split
+(LPG_PERSIST_WG), block size (LPG_DEFER), pricing rule, objective-row count
+(Big-M keeps two) and for runs that start inside a block (lpg_solve's
+growing batches, reads that flush a partial block).
+Reference anchor: the loop is absent upstream (Source/simplex.c:40 -> :65).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle.lpo import GEN_ARTIFICIAL, Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lpg():
+    import linearprogramming_amd as lpg
+    lpg.load()
+    assert lpg.device_count() >= 1, "no GPU visible"
+    return lpg
+
+
+def _log(x):
+    k, r = x.get_log()
+    return list(zip(k.tolist(), r.tolist()))
+
+
+def _engine(lpg, monkeypatch, m, ncols, defer=None, wg=None, persist=None, **kw):
+    env = {"LPG_DEFER": defer, "LPG_PERSIST_WG": wg, "LPG_PERSIST": persist}
+    for k, v in env.items():
+        if v is not None:
+            monkeypatch.setenv(k, str(v))
+    e = lpg.Engine(m, ncols, **kw)
+    for k, v in env.items():
+        if v is not None:
+            monkeypatch.delenv(k)
+    return e
+
+
+def _fits(m, ncols, defer, wg):
+    """block_geometry's rule (lpg_block.hip): <= 256 columns and rows per
+    workgroup, the LDS slices within 150 KB."""
+    if wg is None:
+        return True
+    ncp = (ncols + 1) & ~1
+    cw, rw = -(-ncp // wg), -(-m // wg)
+    s = defer + 8 + ((2 - (defer + 8) % 4) + 4) % 4           # slot_stride
+    return cw <= 256 and rw <= 256 and s * (cw + rw) * 8 <= 150 * 1024
+
+
+def _assert_same(e, o, m):
+    assert _log(e) == _log(o)
+    assert np.array_equal(e.get_basis(), o.get_basis())
+    assert np.array_equal(e.get_rows(0, m + 1), o.get_rows())
+
+
+def test_engaged_where_the_slices_fit(lpg, monkeypatch):
+    e = _engine(lpg, monkeypatch, 600, 1701, defer=32)
+    assert e.info.pivot_wg > 0
+    assert _engine(lpg, monkeypatch, 600, 1701, defer=32, persist=0).info.pivot_wg == 0
+    assert _engine(lpg, monkeypatch, 600, 1701, defer=0).info.pivot_wg == 0      # eager updates
+    # 256 workgroups hold at most 256 columns each: wider tableaus keep the pair
+    assert _engine(lpg, monkeypatch, 8, 256 * 256 + 3, defer=8).info.pivot_wg == 0
+
+
+@pytest.mark.parametrize("wg", [None, 3, 7, 64, 256])
+@pytest.mark.parametrize("defer", [8, 32, 64])
+@pytest.mark.parametrize("m,n,seed,kind,rule", [(200, 300, 12, 0, 0), (48, 48, 14, 1, 1), (257, 100, 15, 1, 0)])
+def test_to_optimality(lpg, monkeypatch, wg, defer, m, n, seed, kind, rule):
+    assert _fits(m, n + m + 1, defer, wg)
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer, wg=wg)
+    assert e.info.pivot_wg > 0
+    o = Oracle(m, n + m + 1)
+    e.generate(n, seed, kind)
+    o.generate(n, seed, kind)
+    res = e.solve(200_000, rule)
+    ores = o.solve(200_000, rule)
+    assert res.status == ores.status == 1
+    assert res.pivots == ores.pivots > 0 and res.objective == ores.objective
+    _assert_same(e, o, m)
+
+
+@pytest.mark.parametrize("wg", [None, 17])
+def test_config2_to_optimality(lpg, monkeypatch, wg):
+    m, n = 1024, 2048
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32, wg=wg)
+    assert e.info.pivot_wg > 0
+    o = Oracle(m, n + m + 1, nthreads=8)
+    e.generate(n, 20220518, 0)
+    o.generate(n, 20220518, 0)
+    res = e.solve(200_000, 0)
+    ores = o.solve(200_000, 0)
+    assert res.status == ores.status == 1 and res.pivots == ores.pivots
+    _assert_same(e, o, m)
+
+
+def test_runs_that_start_inside_a_block(lpg, monkeypatch):
+    """Enqueue 5, 9, 17, ... pivots: every launch after the first starts at a
+    pending index > 0 and reloads the earlier slots' slices from Pbuf / Cbuf;
+    a read in between flushes a partial block."""
+    m, n = 300, 450
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=64)
+    o = Oracle(m, n + m + 1)
+    e.generate(n, 77, 0)
+    o.generate(n, 77, 0)
+    e.reserve_log(4096)
+    total = 0
+    for step in (5, 9, 17, 1, 33, 2, 64, 7):
+        e.enqueue(step, 0)
+        total += step
+        if step == 17:
+            e.get_rows(0, 4)                      # flushes the 31 pending pivots
+    res = e.sync()
+    ores = o.solve(total, 0)
+    assert res.pivots == ores.pivots == total
+    _assert_same(e, o, m)
+
+
+@pytest.mark.parametrize("m,n,rule", [(257, 300, 0), (640, 512, 1)])
+def test_big_m_two_objective_rows(lpg, monkeypatch, m, n, rule):
+    art_first = 1 + n + (m + 1) // 2
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32, flags=lpg._lib.FLAG_BIG_M)
+    assert e.info.pivot_wg > 0 and e.info.nobj == 2
+    o = Oracle(m, n + m + 1, nobj=2)
+    e.generate(n, 9, GEN_ARTIFICIAL)
+    o.generate(n, 9, GEN_ARTIFICIAL)
+    r = e.solve_big_m(art_first, None, 100_000, rule)
+    ro = o.solve_big_m(art_first, None, 100_000, rule)
+    assert r.status == ro.status and r.pivots == ro.pivots > 0 and r.objective == ro.objective
+    assert _log(e) == _log(o)
+    assert np.array_equal(e.get_basis(), o.get_basis())
+    assert np.array_equal(e.get_rows(0, m + 2), o.get_rows())
+
+
+@pytest.mark.parametrize("m,n,piv", [(4096, 8192, 200), (2048, 20000, 150)])
+def test_same_as_two_kernel_pair(lpg, monkeypatch, m, n, piv):
+    """At sizes where the oracle is slow the persistent kernel is checked
+    against the two-kernel pair: same log, same rows (sampled)."""
+    a = _engine(lpg, monkeypatch, m, n + m + 1, defer=64)
+    b = _engine(lpg, monkeypatch, m, n + m + 1, defer=64, persist=0)
+    assert a.info.pivot_wg > 0 and b.info.pivot_wg == 0
+    for e in (a, b):
+        e.generate(n, 5, 0)
+        e.solve(piv, 0)
+    assert _log(a) == _log(b)
+    assert np.array_equal(a.get_basis(), b.get_basis())
+    rows = np.random.default_rng(1).choice(m, 48, replace=False)
+    for i in list(rows) + [m]:
+        assert np.array_equal(a.get_rows(int(i), 1), b.get_rows(int(i), 1))
+
+
+@pytest.mark.parametrize("defer", [8, 64])
+def test_two_kernel_pair_still_bitwise(lpg, monkeypatch, defer):
+    """LPG_PERSIST=0 (and tableaus too wide for the slices, and every
+    communicator) keep k_prep_d / k_select_d: still the oracle's results."""
+    m, n = 200, 300
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer, persist=0)
+    assert e.info.pivot_wg == 0
+    o = Oracle(m, n + m + 1)
+    e.generate(n, 12, 0)
+    o.generate(n, 12, 0)
+    res = e.solve(200_000, 0)
+    ores = o.solve(200_000, 0)
+    assert res.status == ores.status == 1 and res.pivots == ores.pivots
+    _assert_same(e, o, m)
