@@ -218,6 +218,57 @@ int debug_block_phases(unsigned long long *out) {
 #define LPG_BPH(t, k) do { } while (0)
 #endif
 
+// The pending chains of one thread, fully unrolled over NS slots with every
+// LDS read issued before the first fma (one wave per SIMD cannot hide an LDS
+// round trip per step). Slots past the chain read as exact no-ops: past q the
+// slices hold +0 and the multiplier / P_u[k] rows hold -0 / +0.
+// Pivot row, column j: x = fma(m_u, P_u[j], x) for u < q; with SEL the steps
+// u <= qs (the row's restart point, uniform) are (-0, +0) no-ops.
+template <int NS, bool SEL>
+__device__ __forceinline__ double chain_row(const double *sPt, const double *wmw, int qs, double x) {
+    d2 pv[NS / 2], mv[NS / 2];
+#pragma unroll
+    for (int j = 0; j < NS / 2; j++) {
+        pv[j] = ((const d2 *)sPt)[j];
+        mv[j] = ((const d2 *)wmw)[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NS / 2; j++) {
+        if (SEL) {
+            const bool l0 = 2 * j > qs, l1 = 2 * j + 1 > qs;
+            x = fma(l0 ? mv[j].x : -0.0, l0 ? pv[j].x : 0.0, x);
+            x = fma(l1 ? mv[j].y : -0.0, l1 ? pv[j].y : 0.0, x);
+        } else {
+            x = fma(mv[j].x, pv[j].x, x);
+            x = fma(mv[j].y, pv[j].y, x);
+        }
+    }
+    return x;
+}
+// Entering column, row i: x = fma(-C_v[i], P_v[k], x) for v <= q; with SEL
+// the steps v <= lp (this lane's restart point, -1 if none) are (+0, +0) no-ops.
+template <int NS, bool SEL>
+__device__ __forceinline__ double chain_col(const double *sCt, const double *wpw, int lp, double x) {
+    d2 cv[NS / 2], pk[NS / 2];
+#pragma unroll
+    for (int j = 0; j < NS / 2; j++) {
+        cv[j] = ((const d2 *)sCt)[j];
+        pk[j] = ((const d2 *)wpw)[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NS / 2; j++) {
+        if (SEL) {
+            const bool l0 = 2 * j > lp, l1 = 2 * j + 1 > lp;
+            x = fma(-(l0 ? cv[j].x : 0.0), l0 ? pk[j].x : 0.0, x);
+            x = fma(-(l1 ? cv[j].y : 0.0), l1 ? pk[j].y : 0.0, x);
+        } else {
+            x = fma(-cv[j].x, pk[j].x, x);
+            x = fma(-cv[j].y, pk[j].y, x);
+        }
+    }
+    return x;
+}
+
 struct BlockArgs {
     double *T;
     Geo g;
@@ -270,6 +321,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     // ---- launch start: everything here was written before the launch
     int s = a.s0;
     const int32_t status0 = st->slot[s].status;
+    const int64_t np0 = st->pivots, logcap = st->logcap;   // pivots before this launch (workgroup 0 counts on)
     int64_t kt = st->slot[s].k;                        // entering column (logical) of the first pivot
     double cobjM = NOBJ == 2 ? a.Cs0[rM] : 0.0, cobjR = a.Cs0[rR];
     double dM = 0.0, dR = 0.0;
@@ -384,16 +436,17 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             }
             break;
         }
-        if (wg == 0 && tid == 0) {                      // k_prep_d's bookkeeping
+        // k_prep_d's bookkeeping, stores only (a dependent load here would hold
+        // back workgroup 0, and every sweep waits for the slowest workgroup):
+        // the row's owner records the leaving variable it holds
+        if (wg == 0 && tid == 0) {
             st->slot[s].r = r;
             D.rq[q] = r;
             st->npend = q + 1;
             D.kq[q] = kt;
-            D.lv[q] = D.basis[r];
             D.pv[q] = piv;
-            D.basis[r] = kt;
-            const int64_t np = st->pivots;
-            if (D.logk && np < st->logcap) {
+            const int64_t np = np0 + t;
+            if (D.logk && np < logcap) {
                 D.logk[np] = kt;
                 D.logr[np] = r;
             }
@@ -402,6 +455,8 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             st->last_r = r;
         }
         if (hr && i == r) {
+            D.lv[q] = mybasis;
+            D.basis[r] = kt;
             mybasis = kt;
             lastpiv = q;
         }
@@ -412,48 +467,19 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         if (lane == q) rqv = r;
         double x = hc ? g.T[r * g.ld + c] : 0.0;
         LPG_BPH(t, 2);
-        int u = 0;
-        if (qs >= 0) {
-            x = sPt[qs];
-            u = qs + 1;
-        }
-        if ((u & 1) && u < q) {                         // one step to reach an even slot (16-byte reads)
-            x = fma(wm[wave][u], sPt[u], x);
-            u++;
-        }
-        // the pending chain in batches of 8 (slots past q are (P = +0,
-        // multiplier = -0): exact no-ops), the next batch's LDS reads issued
-        // before this batch's fmas
-        if (u < q) {
-            d2 pv[4], mv[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                pv[j] = *(const d2 *)(sPt + u + 2 * j);
-                mv[j] = *(const d2 *)(&wm[wave][u + 2 * j]);
-            }
-            for (;;) {
-                const bool more = u + 8 < q;
-                d2 pn[4], mn[4];
-                if (more) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        pn[j] = *(const d2 *)(sPt + u + 8 + 2 * j);
-                        mn[j] = *(const d2 *)(&wm[wave][u + 8 + 2 * j]);
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    x = fma(mv[j].x, pv[j].x, x);
-                    x = fma(mv[j].y, pv[j].y, x);
-                }
-                if (!more) break;
-                u += 8;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    pv[j] = pn[j];
-                    mv[j] = mn[j];
-                }
-            }
+        // the pending chain over slots u < q (NS >= q), restarting after qs
+        if (qs >= 0) x = sPt[qs];
+        const double *wmw = &wm[wave][0];
+        if (qs < 0) {
+            if (q <= 16) x = chain_row<16, false>(sPt, wmw, qs, x);
+            else if (q <= 32) x = chain_row<32, false>(sPt, wmw, qs, x);
+            else if (q <= 48) x = chain_row<48, false>(sPt, wmw, qs, x);
+            else x = chain_row<64, false>(sPt, wmw, qs, x);
+        } else {
+            if (q <= 16) x = chain_row<16, true>(sPt, wmw, qs, x);
+            else if (q <= 32) x = chain_row<32, true>(sPt, wmw, qs, x);
+            else if (q <= 48) x = chain_row<48, true>(sPt, wmw, qs, x);
+            else x = chain_row<64, true>(sPt, wmw, qs, x);
         }
         drain();                                        // the previous phase's C stores, before this record
         PricePart pb{0.0, -1, 0, 0};
@@ -553,40 +579,23 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             wp[wave][lane] = lane < q ? ld_wt(D.Pbuf + (int64_t)lane * g.ld + kp) : (lane == q ? pkq : 0.0);
         LPG_BPH(t, 6);
         if (hr) b = (i == r) ? p0q : fma(-sCt[q], p0q, b);
-        // the chain in batches of 8 (slots past q are (C = +0, P = +0): exact
-        // no-ops). A row pivoted earlier in this block restarts at its last
-        // pivot lp: x = P_lp[k], and the steps up to lp become (+0, +0) no-ops
-        // (operand selects, off the dependent fma chain).
+        // the chain over slots v <= q (NS > q). A row pivoted earlier in this
+        // block restarts at its last pivot lp: x = P_lp[k] and the steps up to
+        // lp become no-ops (the select form, for waves holding such a row).
         if (hr && lastpiv >= 0) xa = wp[wave][lastpiv];
         {
-            d2 cv[4], pk[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                cv[j] = *(const d2 *)(sCt + 2 * j);
-                pk[j] = *(const d2 *)(&wp[wave][2 * j]);
-            }
-            for (int v = 0;; v += 8) {
-                const bool more = v + 8 <= q;
-                d2 cn[4], pn[4];
-                if (more) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        cn[j] = *(const d2 *)(sCt + v + 8 + 2 * j);
-                        pn[j] = *(const d2 *)(&wp[wave][v + 8 + 2 * j]);
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const bool l0 = v + 2 * j > lastpiv, l1 = v + 2 * j + 1 > lastpiv;
-                    xa = fma(-(l0 ? cv[j].x : 0.0), l0 ? pk[j].x : 0.0, xa);
-                    xa = fma(-(l1 ? cv[j].y : 0.0), l1 ? pk[j].y : 0.0, xa);
-                }
-                if (!more) break;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    cv[j] = cn[j];
-                    pk[j] = pn[j];
-                }
+            const double *wpw = &wp[wave][0];
+            const bool sel = __ballot(hr && lastpiv >= 0) != 0ull;
+            if (!sel) {
+                if (q < 16) xa = chain_col<16, false>(sCt, wpw, lastpiv, xa);
+                else if (q < 32) xa = chain_col<32, false>(sCt, wpw, lastpiv, xa);
+                else if (q < 48) xa = chain_col<48, false>(sCt, wpw, lastpiv, xa);
+                else xa = chain_col<64, false>(sCt, wpw, lastpiv, xa);
+            } else {
+                if (q < 16) xa = chain_col<16, true>(sCt, wpw, lastpiv, xa);
+                else if (q < 32) xa = chain_col<32, true>(sCt, wpw, lastpiv, xa);
+                else if (q < 48) xa = chain_col<48, true>(sCt, wpw, lastpiv, xa);
+                else xa = chain_col<64, true>(sCt, wpw, lastpiv, xa);
             }
         }
         LPG_BPH(t, 7);

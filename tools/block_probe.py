@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import linearprogramming_amd as lpg  # noqa: E402
 
-lib = lpg.load(os.path.join(ROOT, "tools", "liblpg_phases.so"))
+lib = lpg.load(os.path.join(ROOT, "tools", os.environ.get("PHASES_LIB", "liblpg_phases.so")))
 lib.lpg_debug_block_phases.restype = ctypes.c_int
 lib.lpg_debug_block_phases.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 m, n = int(os.environ.get("M", 16384)), int(os.environ.get("N", 32768))
