@@ -211,11 +211,18 @@ __device__ unsigned long long g_bph[2][64][8];
         if (tid == 0 && (wg == 0 || wg == nwg / 2) && (t) < 64)                                \
             g_bph[wg == 0 ? 0 : 1][(t)][(k)] = __builtin_amdgcn_s_memrealtime();               \
     } while (0)
+__device__ unsigned long long g_bpub[2][64][256];   // every workgroup's publish stamp, phase P / S
+#define LPG_BPUB(ph, t)                                                                        \
+    do {                                                                                       \
+        if (tid == 0 && (t) < 64 && wg < 256) g_bpub[ph][(t)][wg] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 int debug_block_phases(unsigned long long *out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bph), sizeof g_bph) == hipSuccess ? 0 : -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bph), sizeof g_bph) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out + sizeof g_bph / 8, HIP_SYMBOL(g_bpub), sizeof g_bpub) == hipSuccess ? 0 : -1;
 }
 #else
 #define LPG_BPH(t, k) do { } while (0)
+#define LPG_BPUB(ph, t) do { } while (0)
 #endif
 
 // The pending chains of one thread, fully unrolled over NS slots with every
@@ -519,6 +526,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             rec_store(recP, (wg * NGP + 2) * 16, pack(0ull, 0u, tag));
             if (NOBJ == 2) rec_store(recP, (wg * NGP + 4) * 16, pack(0ull, 0u, tag));
         }
+        LPG_BPUB(0, t);
         LPG_BPH(t, 3);
 
         // ================= phase S: the entering column and the ratio test
@@ -634,6 +642,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             if (NOBJ == 2) a.Cs1[rM] = nM;
             for (int e = nwg; e < a.ncand; e++) a.part[e] = Cand{0.0, 0.0, -1, -1};
         }
+        LPG_BPUB(1, t);
         LPG_BPH(t, 5);
         kt = kn;
         cobjR = nR;

@@ -27,7 +27,7 @@ e.reserve_log(4 * K + 8)
 e.solve(2 * K, 0)                    # warm: bootstrap + two blocks, flushed
 e.enqueue(K, 0)                      # one launch of K pivots
 torch.cuda.synchronize()
-buf = (ctypes.c_ulonglong * (2 * 64 * 8))()
+buf = (ctypes.c_ulonglong * (2 * 64 * 8 + 2 * 64 * 256))()
 assert lib.lpg_debug_block_phases(buf) == 0
 names = ["P-sweep", "row-load", "P-chain+publish", "S-sweep", "S-load", "S-chain", "S-publish", "->next"]
 for w in (0, 1):
@@ -45,3 +45,20 @@ for w in (0, 1):
         print(f"  t in [{lo:2d},{hi:2d}): " + " ".join(f"{nm}={a / cnt:.2f}" for nm, a in zip(names, acc)) +
               f"  total={sum(acc) / cnt:.2f}")
     print(f"  launch span (wg stamps) {(st[K - 1][5] - st[0][0]) * 0.01:.1f} us for {K} pivots")
+
+# publish skew: per pivot, every workgroup's record-store stamp (phase P and S)
+nwg = e.info.pivot_wg
+base = 2 * 64 * 8
+for ph, nm in ((0, "P"), (1, "S")):
+    spread, late = [], {}
+    for t in range(1, K):
+        v = [buf[base + (ph * 64 + t) * 256 + w] for w in range(nwg)]
+        srt = sorted(v)
+        med = srt[len(srt) // 2]
+        spread.append(((srt[-1] - med) * 0.01, (med - srt[0]) * 0.01))
+        w = v.index(srt[-1])
+        late[w] = late.get(w, 0) + 1
+    import statistics
+    print(f"phase {nm} publish: max-median {statistics.mean(a for a, _ in spread):.2f} us, "
+          f"median-min {statistics.mean(b for _, b in spread):.2f} us; latest workgroups: "
+          + ", ".join(f"{w}x{c}" for w, c in sorted(late.items(), key=lambda x: -x[1])[:8]))
