@@ -307,6 +307,8 @@ def main():
                                                            if world > 1 or a.force_rccl else ""),
                    "update": (f"deferred blocks of {defer} pivots (one k_flush pass per block)" if defer
                               else "eager rank-1 update per pivot"),
+                   "pivot_loop": (f"k_pivot_block: one persistent launch per block, {info.pivot_wg} workgroups"
+                                  if info.pivot_wg else "k_prep_d + k_select_d per pivot"),
                    "update_variant": int(os.environ.get("LPG_UPDATE_VARIANT", "-1"))},
         "roofline": roof,
         "status": lpg.STATUS_NAMES.get(res.status, res.status),

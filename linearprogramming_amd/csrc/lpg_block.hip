@@ -52,6 +52,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "lpg_device.h"
 #include "lpg_internal.h"
 
@@ -660,20 +662,27 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
 
 int block_records_bytes(int nwg) { return nwg * (kRecPMax + kRecR) * 16; }
 
+// Default split: the FEWEST workgroups whose slices fit (one column and one
+// row per thread at most, both slices in LDS). Every per-pivot all-to-all
+// sweeps one record per workgroup, and its cost grows with their number
+// (config 2: 77.6k pivots/s on 256 workgroups, 99.8k on 16; config 5: 58.6k
+// on 256, 65.2k on 128; config 3 needs all 256 for the LDS).
 int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, int *rw, size_t *lds) {
     const int64_t ncp = (g.ncols + 1) & ~(int64_t)1;
-    int w = want > 0 ? want : cus;
-    if (w > kMaxWG) w = kMaxWG;
-    if (w > cus) w = cus;
-    if (w < 1) return -1;
+    const int64_t S = slot_stride(ks);
+    const int64_t per_wg = kMaxLds / (S * (int64_t)sizeof(double));   // columns + rows one workgroup holds
+    int64_t w = want;
+    if (w <= 0) {
+        w = std::max<int64_t>({(ncp + kNT - 1) / kNT, (g.nloc + kNT - 1) / kNT, (ncp + g.nloc + per_wg - 1) / per_wg, 1});
+        while (w <= kMaxWG && w <= cus && ((ncp + w - 1) / w + (g.nloc + w - 1) / w) > per_wg) w++;
+    }
+    if (w > kMaxWG || w > cus || w < 1) return -1;
     const int64_t c = (ncp + w - 1) / w, r = (g.nloc + w - 1) / w;
-    if (c > kNT || r > kNT) return -1;
-    const size_t bytes = (size_t)slot_stride(ks) * (size_t)(c + r) * sizeof(double);
-    if (bytes > (size_t)kMaxLds) return -1;
-    *nwg = w;
+    if (c > kNT || r > kNT || c + r > per_wg) return -1;
+    *nwg = (int)w;
     *cw = (int)c;
     *rw = (int)r;
-    *lds = bytes;
+    *lds = (size_t)(S * (c + r)) * sizeof(double);
     return 0;
 }
 
