@@ -39,6 +39,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import sys
 import time
 
 import linearprogramming_amd as lpg   # first: binds the process to the system ROCm runtime (_lib.bind_runtime)
@@ -70,6 +71,14 @@ def parse():
     ap.add_argument("--variant", type=int, default=None, help="eager update-kernel form (LPG_UPDATE_VARIANT 0|1)")
     ap.add_argument("--no-skip", action="store_true", help="update every column (disable column skipping)")
     ap.add_argument("--force-rccl", action="store_true", help="attach a 1-rank RCCL communicator at N=1 (times the exchange)")
+    ap.add_argument("--exchange", choices=["push", "rccl"], default=os.environ.get("LPG_EXCHANGE", "push"),
+                    help="per-pivot exchange with N>1 (or --force-*): owner push through IPC-mapped buffers "
+                         "(default), or RCCL allreduce + allgather")
+    ap.add_argument("--host-comm", action="store_true",
+                    help="N>1: set up through gloo host collectives instead of RCCL (ranks sharing one GPU, "
+                         "which RCCL refuses)")
+    ap.add_argument("--force-push", action="store_true", help="N=1: attach the owner-push exchange to a 1-rank "
+                                                              "host communicator (times the push kernels)")
     ap.add_argument("--defer", type=int, default=None, help="pivots per deferred block (LPG_DEFER; 0 = eager updates)")
     return ap.parse_args()
 
@@ -108,6 +117,28 @@ def cpu_baseline(m, n, gpu_log, budget_s, budget_1core_s):
             "sample": f"{done} timed pivots (after 1 untimed) of the same {m}x{n} LP, oracle/liblpo.so "
                       f"(C fp64, OpenMP {threads} threads)",
             "seconds": dt, "single_core": one}, {"pivots_compared": int(n_cmp), "identical_pivot_sequence": same}
+
+
+def host_ops(world):
+    """gloo host collectives for lpg_comm_init_host (setup and bootstrap only once the push exchange is attached)."""
+    import numpy as np
+
+    def allgather(b: bytes) -> bytes:
+        if world == 1:
+            return b
+        t = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return b"".join(bytes(o.numpy()) for o in outs)
+
+    def allreduce(arr: "np.ndarray") -> "np.ndarray":
+        if world == 1:
+            return arr
+        t = torch.from_numpy(arr)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.numpy()
+
+    return allgather, allreduce
 
 
 def config5(a):
@@ -184,7 +215,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    result_fd = 1
     if world > 1:
+        # gloo (and RCCL) print connection banners on fd 1; stdout carries exactly
+        # one JSON line, so everything else goes to stderr and the line is
+        # written to the saved descriptor
+        sys.stdout.flush()
+        result_fd = os.dup(1)
+        os.dup2(2, 1)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = CONFIGS[a.config]
@@ -194,19 +232,80 @@ def main():
         raise SystemExit("no GPU visible")
     dev = local % ndev
 
-    eng = lpg.Engine(m, n + m + 1, device=dev, world=world, rank=rank)
-    if world > 1:
-        uid = [lpg.Engine.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng.comm_init_rccl(uid[0])
-    elif a.force_rccl:
-        eng.comm_init_rccl(lpg.Engine.rccl_unique_id())
-    eng.generate(n, SEED, lpg.GEN_DENSE)
+    def make_engine(push):
+        e = lpg.Engine(m, n + m + 1, device=dev, world=world, rank=rank)
+        if world > 1 and not a.host_comm:
+            uid = [lpg.Engine.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            e.comm_init_rccl(uid[0])
+        elif world > 1 or a.force_push:
+            e.comm_init_host(*host_ops(world))
+        elif a.force_rccl:
+            e.comm_init_rccl(lpg.Engine.rccl_unique_id())
+        if push:                                       # every rank attaches it, or none does
+            def agree(ok):
+                if world == 1:
+                    return ok
+                t = torch.tensor([1 if ok else 0], dtype=torch.int64)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                return bool(t.item())
+            try:
+                h = e.push_handle()
+            except lpg.LPGError as ex:
+                print(f"bench: no owner-push buffer ({ex})", file=sys.stderr)
+                h = None
+            hs = [h]
+            if world > 1:
+                hs = [None] * world
+                dist.all_gather_object(hs, h)
+            ok = agree(all(x is not None for x in hs))
+            if ok:
+                try:
+                    e.comm_init_push(hs)
+                except lpg.LPGError as ex:
+                    print(f"bench: owner-push attach failed ({ex})", file=sys.stderr)
+                    ok = False
+                ok = agree(ok)
+            if not ok:
+                e.close()
+                return make_engine(False)
+        e.generate(n, SEED, lpg.GEN_DENSE)
+        return e
+
+    use_push = (world > 1 or a.force_push) and a.exchange == "push"
+    eng = make_engine(use_push)
+    use_push = use_push and eng.info.exchange > 0
     K = eng.info.defer_k or 1                           # pivots per step (one block; eager: one pivot)
     warm, timed = a.warmup * K, a.steps * K
     eng.reserve_log(warm + timed + 8)
-    eng.enqueue(warm, lpg.RULE_DANTZIG)
-    before = eng.sync().pivots
+    failed = 0
+    try:
+        eng.enqueue(warm, lpg.RULE_DANTZIG)
+        before = eng.sync().pivots
+    except lpg.LPGError as ex:                          # the push exchange did not work here: collectives instead
+        if not use_push:
+            raise
+        print(f"bench: owner-push exchange failed in warm-up ({ex}); using the collectives", file=sys.stderr)
+        failed = 1
+    if world > 1:
+        if not failed:                                 # every rank must have taken the same pivots (replicated log)
+            import hashlib
+            lk, lr = eng.get_log()
+            hs = [None] * world
+            dist.all_gather_object(hs, hashlib.sha1(lk.tobytes() + lr.tobytes()).hexdigest())
+            if len(set(hs)) != 1:
+                print("bench: ranks diverged in warm-up; using the collectives", file=sys.stderr)
+                failed = 1
+        ft = torch.tensor([failed], dtype=torch.int64)
+        dist.all_reduce(ft, op=dist.ReduceOp.MAX)
+        failed = int(ft.item())
+    if failed:
+        eng.close()
+        use_push = False
+        eng = make_engine(False)
+        eng.reserve_log(warm + timed + 8)
+        eng.enqueue(warm, lpg.RULE_DANTZIG)
+        before = eng.sync().pivots
 
     # HIP events around the block pass inside the timed region (the roofline
     # numerator's kernel time). For config 2 the events would forbid the
@@ -303,8 +402,11 @@ def main():
                    "tableau_GB": (m + 1) * (n + m + 1) * 8 / 1e9, "rule": "dantzig",
                    "step": (f"one deferred block: {K} pivots + one block pass" if defer else "one pivot (eager)"),
                    "pivots_timed": done,
-                   "parallelism": f"row-block x{world}" + (" (RCCL allgather + allreduce per pivot)"
-                                                           if world > 1 or a.force_rccl else ""),
+                   "parallelism": f"row-block x{world}" + (
+                       (" (owner push per pivot: pivot row and candidates stored into IPC-mapped peer buffers"
+                        + (", uncached" if info.exchange == 2 else "") + ")"
+                        if use_push else " (RCCL allgather + allreduce per pivot)")
+                       if world > 1 or a.force_rccl or a.force_push else ""),
                    "update": (f"deferred blocks of {defer} pivots (one k_flush pass per block)" if defer
                               else "eager rank-1 update per pivot"),
                    "pivot_loop": (f"k_pivot_block: one persistent launch per block, {info.pivot_wg} workgroups"
@@ -324,7 +426,10 @@ def main():
     else:
         line["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        if result_fd == 1:
+            print(json.dumps(line), flush=True)
+        else:
+            os.write(result_fd, (json.dumps(line) + "\n").encode())
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -111,6 +111,9 @@ typedef struct {
                                    pivots, lpg_block.hip); 0: two kernels per pivot */
     double  bytes_per_pivot;    /* algorithmic HBM bytes of one rank-1 update on this rank:
                                    16 * (nrows + nobj) * ncols (one read + one write) */
+    int32_t exchange;           /* per-pivot exchange of a multi-rank context: 0 collectives (or none),
+                                   1 owner push, 2 owner push into uncached exchange buffers */
+    int32_t pad2_;
 } lpg_info_t;
 
 typedef struct {
@@ -147,6 +150,22 @@ int  lpg_comm_unique_id(void *uid, size_t len);              /* RCCL id, len >= 
  * a 1-rank communicator (used to test and time the exchange on one GPU). */
 int  lpg_comm_init_rccl(lpg_ctx *ctx, const void *uid, size_t len);
 int  lpg_comm_init_host(lpg_ctx *ctx, const lpg_host_comm_ops *ops);
+/* Owner-push exchange for the deferred multi-rank loop (the north star's
+ * pivot-row broadcast and candidate all-reduce, SURVEY.md §8(e), without a
+ * collective per pivot): the owner of the pivot row stores it straight into
+ * every rank's exchange buffer and raises per-chunk flags, every rank stores
+ * its ratio candidates into every rank's buffer as self-validating tagged
+ * words. Attach a communicator first (setup and bootstrap still use it),
+ * then give every rank all ranks' buffers: IPC handles between processes
+ * (lpg_comm_push_handle -> exchange -> lpg_comm_init_push), device pointers
+ * between ranks of one process (lpg_comm_push_base -> lpg_comm_init_push_local).
+ * Waits are bounded (2 s): a rank that waits longer ends the solve with
+ * LPG_NUMERIC and lpg_last_error names the exchange. */
+#define LPG_PUSH_HANDLE_BYTES 64
+int  lpg_comm_push_handle(lpg_ctx *ctx, void *handle, size_t len);
+int  lpg_comm_push_base(lpg_ctx *ctx, void **base);
+int  lpg_comm_init_push(lpg_ctx *ctx, const void *handles, size_t len);
+int  lpg_comm_init_push_local(lpg_ctx *ctx, void *const *bases, int world);
 /* Replaces RevokeSMatrix (matrix.c:97-123). NULL is a no-op. */
 void lpg_destroy(lpg_ctx *ctx);
 int  lpg_info(const lpg_ctx *ctx, lpg_info_t *out);

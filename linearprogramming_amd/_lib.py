@@ -41,7 +41,7 @@ class Info(ctypes.Structure):
                 ("row0", ctypes.c_int64), ("nrows", ctypes.c_int64),
                 ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("nobj", ctypes.c_int32), ("defer_k", ctypes.c_int32), ("pivot_wg", ctypes.c_int32),
-                ("bytes_per_pivot", ctypes.c_double)]
+                ("bytes_per_pivot", ctypes.c_double), ("exchange", ctypes.c_int32), ("pad2_", ctypes.c_int32)]
 
 
 class Timing(ctypes.Structure):
@@ -66,6 +66,10 @@ PROTOTYPES = [
     ("lpg_comm_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
     ("lpg_comm_init_rccl", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     ("lpg_comm_init_host", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HostCommOps)]),
+    ("lpg_comm_push_handle", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    ("lpg_comm_push_base", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    ("lpg_comm_init_push", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    ("lpg_comm_init_push_local", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]),
     ("lpg_destroy", None, [ctypes.c_void_p]),
     ("lpg_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Info)]),
     ("lpg_last_error", ctypes.c_char_p, [ctypes.c_void_p]),

@@ -68,6 +68,16 @@ struct lpg_ctx {
     size_t pb_lds = 0;
     void *rec = nullptr;          // its records (zeroed once; tags never repeat within a context)
     uint32_t tag = 0;
+    // owner-push exchange of the multi-rank deferred path (Xch, lpg_internal.h)
+    char *xbuf = nullptr;         // this rank's exchange buffer
+    int64_t xbytes = 0, xoffF = 0, xoffC = 0;
+    int xnblk = 0, xnx = 0;
+    bool xuncached = false;
+    char **xbase = nullptr;       // device array of the world buffers
+    std::vector<void *> xpeer;    // IPC-opened peer buffers (closed at destroy)
+    bool xmode = false;           // attached: per pivot k_prep_d / k_select_d MODE 2, no collective
+    uint32_t xtag = 1;            // next pivot's tag (never repeats within the context)
+    bool x_from_cand = true;      // the next pivot's candidates are in `cand` (after a bootstrap)
     hipStream_t stream = nullptr;
     bool own_stream = false;
     // pivot-loop host state
@@ -390,6 +400,7 @@ static int bootstrap(lpg_ctx *c, int rule) {
     c->par = 0;
     c->booted = true;
     c->boot_rule = rule;
+    c->x_from_cand = true;
     return 0;
 }
 
@@ -406,6 +417,7 @@ static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
     c->par = 0;
     c->booted = true;
     c->boot_rule = rule;
+    c->x_from_cand = true;
     return 0;
 }
 
@@ -498,7 +510,8 @@ static int enqueue(lpg_ctx *c, int64_t npiv, int rule) {
     // timing brackets only the flushes, which stay outside the graph
     const bool timed = c->timing && c->defer_k == 0;
     // a host-callback communicator cannot be captured; RCCL's collectives can
-    const bool comm_ok = !has_comm(c) || (c->nccl && !c->have_hops && c->graph_comm);
+    // (the push exchange's tags are launch arguments: never replayed)
+    const bool comm_ok = !has_comm(c) || (c->nccl && !c->have_hops && c->graph_comm && !c->xmode);
     if (!c->use_graphs || timed || !comm_ok || npiv < 2 * G || (G & 1)) return enqueue_eager(c, npiv, rule);
     int rc;
     if (c->pend) {                           // finish the open block first
@@ -545,6 +558,30 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
             if (launch_pivot_d(L, g, rule, c->st, s, s1, c->part, c->nsel_d, P, c->C[s], c->C[s1], c->pp, c->npp_d,
                                c->basis, D, c->pivot_nt))
                 return fail(c, LPG_ERR_DEVICE, "pivot launch failed");
+            if (++c->pend == c->defer_k && !c->capture_block)
+                if ((rc = flush_launch(c))) return rc;
+            c->par = s1;
+            c->enq++;
+            continue;
+        }
+        if (D.on && c->fast_pivot && c->xmode) {   // deferred, owner-push exchange: two kernels, no collective
+            Xch X;
+            X.base = c->xbase;
+            X.world = c->world;
+            X.rank = c->rank;
+            X.nblk = c->xnblk;
+            X.nx = c->xnx;
+            X.from_cand = c->x_from_cand ? 1 : 0;
+            X.tag = c->xtag;
+            X.offF = c->xoffF;
+            X.offC = c->xoffC;
+            if (launch_prep_x(L, g, rule, c->st, s, c->cand, ncand_d, P, c->C[s], c->pp, c->npp_d, D, X))
+                return fail(c, LPG_ERR_DEVICE, "prep launch failed");
+            if (launch_select_x(L, g, rule, c->st, s, s1, c->C[s], c->C[s1], c->pp, c->npp_d, c->basis, c->part,
+                                c->nsel_d, D, X))
+                return fail(c, LPG_ERR_DEVICE, "select launch failed");
+            c->xtag++;
+            c->x_from_cand = false;
             if (++c->pend == c->defer_k && !c->capture_block)
                 if ((rc = flush_launch(c))) return rc;
             c->par = s1;
@@ -598,6 +635,10 @@ static int read_result(lpg_ctx *c, lpg_result *out, int rule) {
     double z = 0;
     HIPCHK(c, hipMemcpyAsync(&z, c->T + (c->nloc + c->nobj - 1) * c->ld, sizeof z, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (h.stall == 2 || h.stall == 3)
+        return fail(c, LPG_ERR_COMM, "owner-push exchange: rank %d waited > 2 s for the %s (a rank stopped, or the "
+                    "buffers are not shared; LPG_EXCHANGE=rccl keeps the collectives)", c->rank,
+                    h.stall == 2 ? "other ranks' ratio candidates" : "pivot row");
     if (h.stall)
         return fail(c, LPG_ERR_DEVICE,
                     "k_pivot_block: a workgroup waited > 2 s for the others (phase %lld, tag %lld, record %lld "
@@ -871,12 +912,98 @@ int lpg_comm_init_host(lpg_ctx *c, const lpg_host_comm_ops *ops) {
     return 0;
 }
 
+// ---- owner-push exchange ----
+static int ensure_xbuf(lpg_ctx *c) {
+    if (c->xbuf) return 0;
+    if (!(c->defer_k > 0 && c->fast_pivot)) return fail(c, LPG_ERR_STATE, "push exchange needs the deferred pivot pair");
+    c->xnblk = c->npp_d;
+    c->xnx = c->nsel_d;
+    c->xbytes = xch_bytes(c->ld, c->world, c->xnblk, c->xnx, &c->xoffF, &c->xoffC);
+    // uncached: a peer's stores over xGMI land in this GPU's HBM behind its
+    // L2; with L2 out of the path the system-scope loads cannot hit a stale line
+    void *p = nullptr;
+    if (hipExtMallocWithFlags(&p, (size_t)c->xbytes, hipDeviceMallocUncached) == hipSuccess) {
+        c->xuncached = true;
+    } else {
+        (void)hipGetLastError();
+        HIPCHK(c, hipMalloc(&p, (size_t)c->xbytes));
+    }
+    c->xbuf = (char *)p;
+    HIPCHK(c, hipMemset(c->xbuf, 0, (size_t)c->xbytes));
+    return 0;
+}
+
+static int attach_push(lpg_ctx *c, std::vector<char *> &bases) {
+    HIPCHK(c, hipMalloc((void **)&c->xbase, bases.size() * sizeof(char *)));
+    HIPCHK(c, hipMemcpy(c->xbase, bases.data(), bases.size() * sizeof(char *), hipMemcpyHostToDevice));
+    graph_drop(c);
+    c->xmode = true;
+    c->booted = false;               // the next pivot bootstraps (its candidates through the communicator)
+    return 0;
+}
+
+int lpg_comm_push_handle(lpg_ctx *c, void *handle, size_t len) {
+    if (!c || !handle || len < sizeof(hipIpcMemHandle_t)) return fail(c, LPG_ERR_ARG, "push handle buffer too small");
+    if (!has_comm(c)) return fail(c, LPG_ERR_STATE, "attach a communicator before the push exchange");
+    int rc;
+    if ((rc = use_device(c)) || (rc = ensure_xbuf(c))) return rc;
+    hipIpcMemHandle_t h;
+    HIPCHK(c, hipIpcGetMemHandle(&h, c->xbuf));
+    memcpy(handle, &h, sizeof h);
+    return 0;
+}
+
+int lpg_comm_push_base(lpg_ctx *c, void **base) {
+    if (!c || !base) return fail(c, LPG_ERR_ARG, "base is NULL");
+    if (!has_comm(c)) return fail(c, LPG_ERR_STATE, "attach a communicator before the push exchange");
+    int rc;
+    if ((rc = use_device(c)) || (rc = ensure_xbuf(c))) return rc;
+    *base = c->xbuf;
+    return 0;
+}
+
+int lpg_comm_init_push(lpg_ctx *c, const void *handles, size_t len) {
+    if (!c || !handles || len != (size_t)c->world * sizeof(hipIpcMemHandle_t))
+        return fail(c, LPG_ERR_ARG, "need world x %zu handle bytes", sizeof(hipIpcMemHandle_t));
+    if (c->xmode) return fail(c, LPG_ERR_STATE, "push exchange already attached");
+    int rc;
+    if ((rc = use_device(c)) || (rc = ensure_xbuf(c))) return rc;
+    std::vector<char *> bases((size_t)c->world, nullptr);
+    for (int r = 0; r < c->world; r++) {
+        if (r == c->rank) {
+            bases[r] = c->xbuf;
+            continue;
+        }
+        hipIpcMemHandle_t h;
+        memcpy(&h, (const char *)handles + (size_t)r * sizeof h, sizeof h);
+        void *p = nullptr;
+        HIPCHK(c, hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        c->xpeer.push_back(p);
+        bases[r] = (char *)p;
+    }
+    return attach_push(c, bases);
+}
+
+int lpg_comm_init_push_local(lpg_ctx *c, void *const *bases_in, int world) {
+    if (!c || !bases_in || world != c->world) return fail(c, LPG_ERR_ARG, "need world device pointers");
+    if (c->xmode) return fail(c, LPG_ERR_STATE, "push exchange already attached");
+    int rc;
+    if ((rc = use_device(c)) || (rc = ensure_xbuf(c))) return rc;
+    if (bases_in[c->rank] != c->xbuf) return fail(c, LPG_ERR_ARG, "bases[rank] is not this rank's buffer");
+    std::vector<char *> bases((size_t)world);
+    for (int r = 0; r < world; r++) bases[r] = (char *)bases_in[r];
+    return attach_push(c, bases);
+}
+
 void lpg_destroy(lpg_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     graph_drop(c);
     if (c->nccl) rccl_api()->CommDestroy(c->nccl);
+    for (void *p : c->xpeer) (void)hipIpcCloseMemHandle(p);
+    if (c->xbase) (void)hipFree(c->xbase);
+    if (c->xbuf) (void)hipFree(c->xbuf);
     for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
@@ -902,6 +1029,8 @@ int lpg_info(const lpg_ctx *c, lpg_info_t *o) {
     o->defer_k = c->defer_k;
     o->pivot_wg = c->persist ? c->pb_nwg : 0;
     o->bytes_per_pivot = 16.0 * (double)(c->nloc + c->nobj) * (double)c->ncols;
+    o->exchange = c->xmode ? (c->xuncached ? 2 : 1) : 0;
+    o->pad2_ = 0;
     return 0;
 }
 
@@ -1043,7 +1172,7 @@ int lpg_prepare(lpg_ctx *c, int rule) {
     // the conditions under which enqueue replays graphs (enqueue, above)
     const int G = graph_len(c);
     const bool timed = c->timing && c->defer_k == 0;
-    const bool comm_ok = !has_comm(c) || (c->nccl && !c->have_hops && c->graph_comm);
+    const bool comm_ok = !has_comm(c) || (c->nccl && !c->have_hops && c->graph_comm && !c->xmode);
     if (!c->use_graphs || timed || !comm_ok || (G & 1)) return 0;
     if (c->graph[c->par] && c->graph_rule[c->par] == rule) return 0;
     if ((rc = graph_build(c, rule))) {

@@ -72,6 +72,25 @@ struct Defer {
     int      on;
 };
 
+// Owner-push exchange of the multi-rank deferred path (k_prep_d / k_select_d
+// MODE 2, lpg_kernels.hip). Every rank owns one exchange buffer, mapped into
+// every rank's process (IPC between processes, plain device pointers between
+// ranks that share one), laid out as
+//   [0, offF)      xP[2][ld]             the pivot row its owner pushed (by tag parity)
+//   [offF, offC)   xF[2][nblk] (u32)     per prep block: the tag of the P chunk that landed
+//   [offC, ...)    xC[2][world][nx][6]   every rank's ratio candidates, 6 {payload, tag} words each
+// Tags come from a host counter that never repeats within a context; the
+// P chunks are published by a flag behind a system-scope release, the
+// candidates are self-validating 8-byte {payload, tag} words.
+struct Xch {
+    char *const *base;            // device array: the world buffers ([rank] = this rank's own)
+    int world, rank;
+    int nblk, nx;                 // prep blocks (P chunks) and ratio candidates per rank
+    int from_cand;                // 1: this pivot's candidates are in `cand` (after a bootstrap), not in xC
+    uint32_t tag;                 // this pivot's tag (its candidates, its P flags); select publishes tag + 1
+    int64_t offF, offC;           // byte offsets of xF and xC (xP at 0)
+};
+
 // Ratio-test candidate: lexicographic (theta, key); row < 0 = none.
 struct Cand {                 // 32 B
     double  theta;
@@ -136,6 +155,16 @@ int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s,
 // allreduce of P and launch_price(mode 1), then launch_select_dm.
 int launch_prep_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s, const Cand *cand, int ncand,
                    double *P, const double *Cs, int npp_d, const Defer &D);
+// ... or, with the owner-push exchange, these two alone per pivot: prep takes
+// the candidates from every rank's push (or `cand` after a bootstrap), the
+// owner pushes P to every rank, every rank prices (k_price's work fused);
+// select pushes its candidates to every rank.
+int launch_prep_x(const Launch &L, const Geo &g, int rule, DevState *st, int s, const Cand *cand, int ncand,
+                  double *P, const double *Cs, PricePart *pp, int npp_d, const Defer &D, const Xch &X);
+int launch_select_x(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, const double *Cs,
+                    double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part, int nsel,
+                    const Defer &D, const Xch &X);
+int64_t xch_bytes(int64_t ld, int world, int nblk, int nx, int64_t *offF, int64_t *offC);
 int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, const double *Cs,
                      double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part, int nsel,
                      const Defer &D);

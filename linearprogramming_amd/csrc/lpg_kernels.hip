@@ -599,14 +599,68 @@ __device__ unsigned long long g_ph[2][16];
 #define LPG_PH(kern, k) do { } while (0)
 #endif
 
-// MR (multi-rank): the pivot row lives on one rank; the owner computes P,
-// every other rank writes -0 (the identity of the allreduce that follows, so
-// the sum is the owner's row bit for bit, signed zeros included), and the
-// pricing runs after the exchange (k_price), not here.
-template <int RULE, int kPF, int NT, bool MR>
+// ---- owner-push exchange (Xch, lpg_internal.h) ----
+__device__ __forceinline__ void st_sys64(void *p, uint64_t v) {
+    __hip_atomic_store((unsigned long long *)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys64(const void *p) {
+    return (uint64_t)__hip_atomic_load((unsigned long long *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t *xch_flag(const Xch &X, int rank, int par, int b) {
+    return (uint32_t *)(X.base[rank] + X.offF) + (int64_t)par * X.nblk + b;
+}
+__device__ __forceinline__ uint64_t *xch_cand(const Xch &X, int rank, int par, int from, int e) {
+    return (uint64_t *)(X.base[rank] + X.offC) + (((int64_t)par * X.world + from) * X.nx + e) * 6;
+}
+constexpr long long kXSpinTicks = 200000000ll;     // s_memrealtime (100 MHz): 2 s, then NUMERIC + stall
+
+// The candidates of every rank for this pivot (tag X.tag), polled by the
+// whole block until every word carries the tag; false on timeout.
+template <int NT>
+__device__ bool xch_gather(const Xch &X, Cand &best) {
+    const int par = X.tag & 1, n = X.world * X.nx;
+    const long long t0 = (long long)wall_clock64();
+    for (;;) {
+        bool ok = true;
+        Cand b{0.0, 0.0, 0, -1};
+        for (int e = threadIdx.x; e < n; e += NT) {
+            const uint64_t *w = xch_cand(X, X.rank, par, e / X.nx, e % X.nx);
+            uint64_t v[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) v[k] = ld_sys64(w + k);
+#pragma unroll
+            for (int k = 0; k < 6; k++) ok = ok && (uint32_t)(v[k] >> 32) == X.tag;
+            Cand c;
+            c.theta = __longlong_as_double((long long)(((v[1] & 0xffffffffull) << 32) | (v[0] & 0xffffffffull)));
+            c.piv = __longlong_as_double((long long)(((v[3] & 0xffffffffull) << 32) | (v[2] & 0xffffffffull)));
+            c.key = (int64_t)(int32_t)(uint32_t)v[4];
+            c.row = (int64_t)(int32_t)(uint32_t)v[5];
+            if (cand_better(c, b)) b = c;
+        }
+        if (__syncthreads_and(ok)) {
+            best = b;
+            return true;
+        }
+        if ((long long)wall_clock64() - t0 > kXSpinTicks) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// MODE 0 (one rank): pricing fused. MODE 1 (multi-rank, allreduce): the
+// pivot row lives on one rank; the owner computes P, every other rank writes
+// -0 (the identity of the allreduce that follows, so the sum is the owner's
+// row bit for bit, signed zeros included), and the pricing runs after the
+// exchange (k_price), not here. MODE 2 (multi-rank, owner push): the
+// candidates come from every rank's push, the owner stores its P chunk into
+// every other rank's xP and raises that chunk's flag, every other rank's
+// block waits for its chunk's flag and reads it; then every rank prices
+// (k_price's work, fused as in MODE 0).
+template <int RULE, int kPF, int NT, int MODE>
 __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, DevState *st, int s,
                                                    const Cand *__restrict__ cand, int ncand, double *__restrict__ P,
-                                                   const double *__restrict__ Cs, PricePart *__restrict__ pp, Defer D) {
+                                                   const double *__restrict__ Cs, PricePart *__restrict__ pp, Defer D,
+                                                   Xch X) {
+    constexpr bool MR = MODE != 0;
     const int64_t j2 = (int64_t)blockIdx.x * NT + threadIdx.x;
     const int64_t nvec = (g.ncols + 1) / 2;
     const bool col = j2 < nvec;
@@ -616,9 +670,11 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
     // ---- round 1: nothing here depends on the leaving row
     const int32_t status = st->slot[s].status;
     Cand best{0.0, 0.0, 0, -1};
-    for (int q = threadIdx.x; q < ncand; q += NT) {
-        const Cand c = cand[q];
-        if (cand_better(c, best)) best = c;
+    if (MODE != 2 || X.from_cand) {
+        for (int q = threadIdx.x; q < ncand; q += NT) {
+            const Cand c = cand[q];
+            if (cand_better(c, best)) best = c;
+        }
     }
     d2 dM = d2{0.0, 0.0}, dR = d2{0.0, 0.0};
     if (col) {
@@ -639,6 +695,13 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
     const int64_t rqv = lane < D.q ? D.rq[lane] : -1;   // lane q of every wave holds r_q
     const int2 lj = col ? ((const int2 *)D.colmap)[j2] : int2{0, 0};   // logical indices of the two columns
     if (status != RUNNING) return;
+    if (MODE == 2 && !X.from_cand && !xch_gather<NT>(X, best)) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->slot[s].status = NUMERIC;
+            st->stall = 2;
+        }
+        return;
+    }
     LPG_PH(0, 1);
     best = block_argmin_cand<NT / 64>(best);
     LPG_PH(0, 2);
@@ -713,15 +776,66 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
             t.y = fma(c, v.y, t.y);
         }
     }
-    if (MR) {
+    if (MODE == 1) {
         if (col) *(d2 *)(P + 2 * j2) = own ? d2{t.x / best.piv, t.y / best.piv} : d2{-0.0, -0.0};
         return;
     }
+    d2 p = d2{0.0, 0.0};
+    if (col && own) {
+        p.x = t.x / best.piv;
+        p.y = t.y / best.piv;
+    }
+    if (MODE == 2) {
+        const int par = X.tag & 1;
+        if (own) {                 // push this block's chunk to every other rank, then its flag
+            if (col)
+                for (int rk = 0; rk < X.world; rk++) {
+                    if (rk == X.rank) continue;
+                    double *xp = (double *)X.base[rk] + (int64_t)par * g.ld + 2 * j2;
+                    st_sys64(xp, (uint64_t)__double_as_longlong(p.x));
+                    st_sys64(xp + 1, (uint64_t)__double_as_longlong(p.y));
+                }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __threadfence_system();
+                for (int rk = 0; rk < X.world; rk++)
+                    if (rk != X.rank)
+                        __hip_atomic_store(xch_flag(X, rk, par, blockIdx.x), X.tag, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        } else {                   // wait for this block's chunk from the owner
+            __shared__ int xok;
+            if (threadIdx.x == 0) {
+                const long long t0 = (long long)wall_clock64();
+                int ok = 1;
+                while (__hip_atomic_load(xch_flag(X, X.rank, par, blockIdx.x), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM) != X.tag) {
+                    if ((long long)wall_clock64() - t0 > kXSpinTicks) {
+                        ok = 0;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                __threadfence_system();
+                xok = ok;
+            }
+            __syncthreads();
+            if (!xok) {
+                if (threadIdx.x == 0) {
+                    st->slot[s].status = NUMERIC;
+                    st->stall = 3;
+                }
+                return;
+            }
+            if (col) {
+                const double *xp = (const double *)X.base[X.rank] + (int64_t)par * g.ld + 2 * j2;
+                p.x = __longlong_as_double((long long)ld_sys64(xp));
+                p.y = __longlong_as_double((long long)ld_sys64(xp + 1));
+            }
+        }
+    }
     if (col) {
-        const double piv = best.piv;
-        d2 p;
-        p.x = t.x / piv;
-        p.y = t.y / piv;
         *(d2 *)(P + 2 * j2) = p;
         dM.x = fma(cM, p.x, dM.x);
         dM.y = fma(cM, p.y, dM.y);
@@ -741,12 +855,14 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
     LPG_PH(0, 5);
 }
 
-template <int RULE, int kPF, int NT>
+// PUSH (owner-push exchange, Xch): each block also stores its candidate into
+// every rank's xC as 6 self-validating {payload, tag + 1} words.
+template <int RULE, int kPF, int NT, bool PUSH>
 __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, Geo g, DevState *st, int s,
                                                      int s1, const double *__restrict__ Cs, double *__restrict__ Cs1,
                                                      const PricePart *__restrict__ pp, int npp,
                                                      const int64_t *__restrict__ basis, Cand *__restrict__ part,
-                                                     Defer D) {
+                                                     Defer D, Xch X) {
     const int64_t nrows = g.nloc + g.nobj;
     const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;   // one row per thread (launcher checks)
     const bool row = i < nrows;
@@ -884,6 +1000,17 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
     LPG_PH(1, 4);
     best = block_argmin_cand<NT / 64>(best);
     if (threadIdx.x == 0) part[blockIdx.x] = best;
+    if (PUSH && threadIdx.x == 0) {
+        const uint32_t tg = X.tag + 1;
+        const uint64_t th = (uint64_t)__double_as_longlong(best.theta), pv = (uint64_t)__double_as_longlong(best.piv);
+        const uint32_t w[6] = {(uint32_t)th, (uint32_t)(th >> 32), (uint32_t)pv, (uint32_t)(pv >> 32),
+                               (uint32_t)best.key, (uint32_t)best.row};
+        for (int rk = 0; rk < X.world; rk++) {
+            uint64_t *d = xch_cand(X, rk, tg & 1, X.rank, blockIdx.x);
+#pragma unroll
+            for (int k = 0; k < 6; k++) st_sys64(d + k, ((uint64_t)tg << 32) | w[k]);
+        }
+    }
     LPG_PH(1, 5);
 }
 
@@ -913,12 +1040,13 @@ int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s,
     // are not offered.
     if (nt != 256 || npp != pivot_d_blocks(g, 0, nt) || nsel != pivot_d_blocks(g, 1, nt)) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
+    const Xch X0{};
 #define LPG_PD(R, PF, NT)                                                                                             \
     do {                                                                                                              \
-        hipLaunchKernelGGL((k_prep_d<R, PF, NT, false>), dim3(npp), dim3(NT), 0, stream, g.T, g, st, s, part, nsel, P, \
-                           Cs, pp, D);                                                                                \
-        hipLaunchKernelGGL((k_select_d<R, PF, NT>), dim3(nsel), dim3(NT), 0, stream, g.T, g, st, s, s1, Cs, Cs1, pp,   \
-                           npp, basis, part, D);                                                                      \
+        hipLaunchKernelGGL((k_prep_d<R, PF, NT, 0>), dim3(npp), dim3(NT), 0, stream, g.T, g, st, s, part, nsel, P,     \
+                           Cs, pp, D, X0);                                                                            \
+        hipLaunchKernelGGL((k_select_d<R, PF, NT, false>), dim3(nsel), dim3(NT), 0, stream, g.T, g, st, s, s1, Cs, Cs1, \
+                           pp, npp, basis, part, D, X0);                                                              \
     } while (0)
 #define LPG_PD_NT(R, PF)                   \
     do {                                   \
@@ -949,9 +1077,10 @@ int launch_prep_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s,
                    double *P, const double *Cs, int npp_d, const Defer &D) {
     if (npp_d != pivot_d_blocks(g, 0, 256)) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
+    const Xch X0{};
 #define LPG_PM(R, PF)                                                                                                 \
-    hipLaunchKernelGGL((k_prep_d<R, PF, 256, true>), dim3(npp_d), dim3(256), 0, stream, g.T, g, st, s, cand, ncand, P, \
-                       Cs, nullptr, D)
+    hipLaunchKernelGGL((k_prep_d<R, PF, 256, 1>), dim3(npp_d), dim3(256), 0, stream, g.T, g, st, s, cand, ncand, P,    \
+                       Cs, nullptr, D, X0)
     const int pf = D.q < 16 ? 16 : D.q < 32 ? 32 : D.q < 48 ? 48 : 64;   // as launch_pivot_d
     if (rule == RULE_BLAND) {
         if (pf == 16) LPG_PM(RULE_BLAND, 16);
@@ -975,9 +1104,10 @@ int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int 
                      const Defer &D) {
     if ((int64_t)nsel * 256 < g.nloc + g.nobj) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
+    const Xch X0{};
 #define LPG_SM(R, PF)                                                                                               \
-    hipLaunchKernelGGL((k_select_d<R, PF, 256>), dim3(nsel), dim3(256), 0, stream, g.T, g, st, s, s1, Cs, Cs1, pp, \
-                       npp, basis, part, D)
+    hipLaunchKernelGGL((k_select_d<R, PF, 256, false>), dim3(nsel), dim3(256), 0, stream, g.T, g, st, s, s1, Cs, Cs1, \
+                       pp, npp, basis, part, D, X0)
     const int pf = D.q < 16 ? 16 : D.q < 32 ? 32 : D.q < 48 ? 48 : 64;   // as launch_pivot_d
     if (rule == RULE_BLAND) {
         if (pf == 16) LPG_SM(RULE_BLAND, 16);
@@ -991,6 +1121,62 @@ int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int 
         else LPG_SM(RULE_DANTZIG, 64);
     }
 #undef LPG_SM
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Owner-push exchange: the buffer's size and the offsets of its parts (256-byte aligned).
+int64_t xch_bytes(int64_t ld, int world, int nblk, int nx, int64_t *offF, int64_t *offC) {
+    const int64_t f = (2 * ld * (int64_t)sizeof(double) + 255) & ~(int64_t)255;
+    const int64_t c = (f + 2 * (int64_t)nblk * 4 + 255) & ~(int64_t)255;
+    if (offF) *offF = f;
+    if (offC) *offC = c;
+    return c + 2 * (int64_t)world * nx * 6 * 8;
+}
+
+int launch_prep_x(const Launch &L, const Geo &g, int rule, DevState *st, int s, const Cand *cand, int ncand,
+                  double *P, const double *Cs, PricePart *pp, int npp_d, const Defer &D, const Xch &X) {
+    if (npp_d != pivot_d_blocks(g, 0, 256) || X.nblk != npp_d) return -1;
+    hipStream_t stream = (hipStream_t)L.stream;
+#define LPG_PX(R, PF)                                                                                                 \
+    hipLaunchKernelGGL((k_prep_d<R, PF, 256, 2>), dim3(npp_d), dim3(256), 0, stream, g.T, g, st, s, cand, ncand, P,    \
+                       Cs, pp, D, X)
+    const int pf = D.q < 16 ? 16 : D.q < 32 ? 32 : D.q < 48 ? 48 : 64;   // as launch_pivot_d
+    if (rule == RULE_BLAND) {
+        if (pf == 16) LPG_PX(RULE_BLAND, 16);
+        else if (pf == 32) LPG_PX(RULE_BLAND, 32);
+        else if (pf == 48) LPG_PX(RULE_BLAND, 48);
+        else LPG_PX(RULE_BLAND, 64);
+    } else {
+        if (pf == 16) LPG_PX(RULE_DANTZIG, 16);
+        else if (pf == 32) LPG_PX(RULE_DANTZIG, 32);
+        else if (pf == 48) LPG_PX(RULE_DANTZIG, 48);
+        else LPG_PX(RULE_DANTZIG, 64);
+    }
+#undef LPG_PX
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_select_x(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, const double *Cs,
+                    double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part, int nsel,
+                    const Defer &D, const Xch &X) {
+    if ((int64_t)nsel * 256 < g.nloc + g.nobj || nsel != X.nx) return -1;
+    hipStream_t stream = (hipStream_t)L.stream;
+#define LPG_SX(R, PF)                                                                                              \
+    hipLaunchKernelGGL((k_select_d<R, PF, 256, true>), dim3(nsel), dim3(256), 0, stream, g.T, g, st, s, s1, Cs, Cs1, \
+                       pp, npp, basis, part, D, X)
+    const int pf = D.q < 16 ? 16 : D.q < 32 ? 32 : D.q < 48 ? 48 : 64;
+    if (rule == RULE_BLAND) {
+        if (pf == 16) LPG_SX(RULE_BLAND, 16);
+        else if (pf == 32) LPG_SX(RULE_BLAND, 32);
+        else if (pf == 48) LPG_SX(RULE_BLAND, 48);
+        else LPG_SX(RULE_BLAND, 64);
+    } else {
+        if (pf == 16) LPG_SX(RULE_DANTZIG, 16);
+        else if (pf == 32) LPG_SX(RULE_DANTZIG, 32);
+        else if (pf == 48) LPG_SX(RULE_DANTZIG, 48);
+        else LPG_SX(RULE_DANTZIG, 64);
+    }
+#undef LPG_SX
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -154,6 +154,28 @@ class Engine:
         self._keep += [ops, _ag, _ar]
         self._check(self.lib.lpg_comm_init_host(self._ctx, ctypes.byref(ops)), "lpg_comm_init_host")
 
+    # owner-push exchange (include/lpg.h): after a communicator
+    def push_handle(self) -> bytes:
+        buf = ctypes.create_string_buffer(64)
+        self._check(self.lib.lpg_comm_push_handle(self._ctx, buf, 64), "lpg_comm_push_handle")
+        return buf.raw
+
+    def push_base(self) -> int:
+        p = ctypes.c_void_p()
+        self._check(self.lib.lpg_comm_push_base(self._ctx, ctypes.byref(p)), "lpg_comm_push_base")
+        return p.value
+
+    def comm_init_push(self, handles):
+        """handles: every rank's push_handle(), in rank order."""
+        blob = b"".join(bytes(h) for h in handles)
+        buf = ctypes.create_string_buffer(blob, len(blob))
+        self._check(self.lib.lpg_comm_init_push(self._ctx, buf, len(blob)), "lpg_comm_init_push")
+
+    def comm_init_push_local(self, bases):
+        """bases: every rank's push_base() (ranks of one process), in rank order."""
+        arr = (ctypes.c_void_p * len(bases))(*bases)
+        self._check(self.lib.lpg_comm_init_push_local(self._ctx, arr, len(bases)), "lpg_comm_init_push_local")
+
     # -- loading ---------------------------------------------------------
     def load_rows(self, row0: int, rows: np.ndarray):
         rows = np.ascontiguousarray(rows, dtype=np.float64)

@@ -172,3 +172,27 @@ def test_two_kernel_pair_still_bitwise(lpg, monkeypatch, defer):
     ores = o.solve(200_000, 0)
     assert res.status == ores.status == 1 and res.pivots == ores.pivots
     _assert_same(e, o, m)
+
+
+def test_reload_into_a_solved_context(lpg, monkeypatch):
+    """Solve, load a different tableau into the same context (its pending
+    block flushed and its column order restored first), solve again: both
+    solves equal the oracle's (lpg_load_rows after pivoting)."""
+    m, n = 220, 330
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32)
+    assert e.info.pivot_wg > 0
+    o = Oracle(m, n + m + 1)
+    e.generate(n, 31, 0)
+    o.generate(n, 31, 0)
+    e.solve(45, 0)                                  # stops inside a block: 13 pivots pending
+    o.solve(45, 0)
+    _assert_same(e, o, m)
+    o2 = Oracle(m, n + m + 1)
+    o2.generate(n, 32, 0)                           # another LP, loaded through the host path
+    T = o2.get_rows()
+    basis = np.arange(n + 1, n + m + 1, dtype=np.int64)
+    e.load_tableau(T, basis)
+    r2 = e.solve(200_000, 0)
+    ro2 = o2.solve(200_000, 0)
+    assert r2.status == ro2.status == 1 and r2.objective == ro2.objective
+    assert np.array_equal(e.get_rows(0, m + 1), o2.get_rows())

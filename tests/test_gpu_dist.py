@@ -51,7 +51,7 @@ class ThreadComm:
         return acc
 
 
-def _run_threads(lpg, world, m, n, seed, kind, rule, max_pivots):
+def _run_threads(lpg, world, m, n, seed, kind, rule, max_pivots, push=False):
     comm = ThreadComm(world)
     out = [None] * world
     errs = []
@@ -60,6 +60,10 @@ def _run_threads(lpg, world, m, n, seed, kind, rule, max_pivots):
         try:
             e = lpg.Engine(m, n + m + 1, world=world, rank=rank)
             e.comm_init_host(lambda b: comm.allgather(rank, b), lambda a: comm.allreduce(rank, a))
+            if push:                              # owner-push exchange between the threads' buffers
+                mine = e.push_base().to_bytes(8, "little")
+                allb = comm.allgather(rank, mine)
+                e.comm_init_push_local([int.from_bytes(allb[8 * r:8 * r + 8], "little") for r in range(world)])
             e.generate(n, seed, kind)
             res = e.solve(max_pivots, rule)
             info = e.info
@@ -108,7 +112,9 @@ def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule, defer, monk
     assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
 
 
-def _gloo_worker(rank, world, port, m, n, seed, outdir):
+def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule=0, defer=None):
+    if defer is not None:
+        os.environ["LPG_DEFER"] = defer
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -129,35 +135,56 @@ def _gloo_worker(rank, world, port, m, n, seed, outdir):
 
     e = lpg.Engine(m, n + m + 1, world=world, rank=rank)
     e.comm_init_host(allgather, allreduce)
-    e.generate(n, seed, 0)
-    res = e.solve(5000, 0)
+    if push:                                      # owner-push exchange through IPC handles
+        h = allgather(e.push_handle())
+        e.comm_init_push([h[64 * r:64 * r + 64] for r in range(world)])
+    e.generate(n, seed, kind)
+    res = e.solve(5000, rule)
     info = e.info
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
-        pickle.dump(dict(status=res.status, pivots=res.pivots, log=e.get_log(),
+        pickle.dump(dict(status=res.status, pivots=res.pivots, log=e.get_log(), basis=e.get_basis(),
                          rows=e.get_rows(info.row0, info.nrows), obj=e.get_rows(m, 1)[0]), f)
     e.close()
     dist.destroy_process_group()
 
 
-def test_two_processes_gloo_bitwise(lpg):
+def _processes(world, m, n, seed, push, kind=0, rule=0, defer=None):
     import torch.multiprocessing as mp
-    m, n, seed = 120, 200, 31
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_gloo_worker, args=(2, port, m, n, seed, d), nprocs=2, join=True)
-        parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(2)]
+        mp.spawn(_gloo_worker, args=(world, port, m, n, seed, d, push, kind, rule, defer), nprocs=world, join=True)
+        parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     o = Oracle(m, n + m + 1)
-    o.generate(n, seed, 0)
-    ores = o.solve(5000, 0)
+    o.generate(n, seed, kind)
+    ores = o.solve(5000, rule)
     T = o.get_rows()
     for p in parts:
         assert p["status"] == ores.status and p["pivots"] == ores.pivots
-        assert np.array_equal(p["log"][0], o.get_log()[0])
+        assert np.array_equal(p["log"][0], o.get_log()[0]) and np.array_equal(p["log"][1], o.get_log()[1])
+        assert np.array_equal(p["basis"], o.get_basis())
         assert np.array_equal(p["obj"], T[m])
     assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
+
+
+def test_two_processes_gloo_bitwise(lpg):
+    _processes(2, 120, 200, 31, push=False)
+
+
+@pytest.mark.parametrize("world,m,n,kind,rule,defer", [(2, 120, 200, 0, 0, None), (2, 96, 160, 0, 0, "5"),
+                                                       (3, 101, 77, 0, 0, "64"), (2, 64, 64, 1, 1, "5"),
+                                                       (3, 203, 301, 0, 0, "32")])
+def test_processes_owner_push_bitwise(lpg, world, m, n, kind, rule, defer):
+    """The owner-push exchange between ranks in separate processes sharing the
+    GPU (IPC-mapped exchange buffers, the layout of one process per GPU): no
+    collective per pivot -- the owner stores the pivot row into every rank's
+    buffer, every rank its candidates -- bitwise the oracle. (Ranks as threads
+    of one process are not used here: a process gets GPU_MAX_HW_QUEUES = 4
+    hardware queues, and two ranks' streams on one queue would serialise a
+    waiting kernel in front of the kernel it waits for.)"""
+    _processes(world, m, n, 778, push=True, kind=kind, rule=rule, defer=defer)
 
 
 @pytest.mark.parametrize("m,n,defer,graphs", [(300, 500, None, "0"), (1024, 2048, None, "0"), (1024, 2048, "64", "0"),
@@ -192,3 +219,23 @@ def test_host_comm_single_rank(lpg):
     assert res.pivots == ores.pivots and np.array_equal(e.get_rows(0, 51), o.get_rows())
     with pytest.raises(lpg.LPGError):
         e.comm_init_host(lambda b: b, lambda a: a)     # one communicator per context
+
+
+@pytest.mark.parametrize("m,n", [(300, 500), (1024, 2048)])
+def test_owner_push_single_rank(lpg, m, n, monkeypatch):
+    """The owner-push kernels on a 1-rank communicator (pushes to itself):
+    bitwise the engine without a communicator and the oracle."""
+    monkeypatch.setenv("LPG_DEFER", "64")
+    e = lpg.Engine(m, n + m + 1)
+    e.comm_init_host(lambda b: b, lambda a: a)
+    e.comm_init_push([e.push_handle()])
+    assert e.info.exchange in (1, 2)                # 2: the exchange buffer is uncached (hipDeviceMallocUncached)
+    print(f"exchange mode {e.info.exchange}")
+    e.generate(n, 43, 0)
+    res = e.solve(100_000, 0)
+    o = Oracle(m, n + m + 1)
+    o.generate(n, 43, 0)
+    ores = o.solve(100_000, 0)
+    assert res.status == ores.status == 1 and res.pivots == ores.pivots and res.objective == ores.objective
+    assert np.array_equal(e.get_log()[0], o.get_log()[0]) and np.array_equal(e.get_log()[1], o.get_log()[1])
+    assert np.array_equal(e.get_rows(0, m + 1), o.get_rows())
