@@ -431,11 +431,10 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         __syncthreads();
         LPG_BPH(t, 1);
         const int okP = bc.ok;
-        const double theta = __longlong_as_double((long long)bc.h);
         const double piv = __longlong_as_double((long long)bc.p0);
         const int64_t r = (int64_t)bc.p1;               // leaving row (local == global: one rank)
         __syncthreads();                                // bc is rewritten by the next phase
-        if (okP <= 0 || !isfinite(piv) || !isfinite(theta)) {
+        if (okP <= 0 || !isfinite(piv)) {               // the oracle's NUMERIC rule (k_prep_d)
             if (wg == 0 && tid == 0) {
                 const int32_t sv = okP < 0 ? NUMERIC : (okP == 0 ? UNBOUNDED : NUMERIC);
                 st->slot[s].status = sv;
@@ -621,7 +620,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             }
             if (xa > g.eps_piv) {
                 cd.theta = b > 0.0 ? b / xa : 0.0;
-                cd.piv = xa;
+                cd.piv = isfinite(b) ? xa : __longlong_as_double(0x7ff8000000000000ll);   // NUMERIC at phase P
                 cd.row = g.row0 + i;
                 cd.key = RULE == RULE_BLAND ? mybasis : g.row0 + i;
             }

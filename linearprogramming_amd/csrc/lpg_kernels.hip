@@ -256,7 +256,10 @@ __global__ __launch_bounds__(kBlock) void k_prep(double *__restrict__ T, Geo g, 
         if (cand_better(c, best)) best = c;
     }
     best = block_reduce_cand(best);
-    if (best.row < 0 || !isfinite(best.piv) || !isfinite(best.theta)) {
+    // the oracle's rule (oracle/lpo.c lpo_solve): NUMERIC iff the pivot element or
+    // the row's b is not finite (a non-finite b arrives as piv = NaN); an
+    // overflowing ratio b / a is an ordinary (largest) candidate
+    if (best.row < 0 || !isfinite(best.piv)) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->slot[s].status = best.row < 0 ? UNBOUNDED : NUMERIC;
             st->slot[s].r = -1;
@@ -536,7 +539,7 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
             const int64_t grow = g.row0 + i;
             Cand c;
             c.theta = b > 0.0 ? b / a : 0.0;
-            c.piv = a;
+            c.piv = isfinite(b) ? a : __longlong_as_double(0x7ff8000000000000ll);   // b_r not finite: NUMERIC at prep
             c.row = grow;
             c.key = RULE == RULE_BLAND ? (grow == r ? kc : basis[grow]) : grow;
             if (cand_better(c, best)) best = c;
@@ -705,7 +708,10 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
     LPG_PH(0, 1);
     best = block_argmin_cand<NT / 64>(best);
     LPG_PH(0, 2);
-    if (best.row < 0 || !isfinite(best.piv) || !isfinite(best.theta)) {
+    // the oracle's rule (oracle/lpo.c lpo_solve): NUMERIC iff the pivot element or
+    // the row's b is not finite (a non-finite b arrives as piv = NaN); an
+    // overflowing ratio b / a is an ordinary (largest) candidate
+    if (best.row < 0 || !isfinite(best.piv)) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->slot[s].status = best.row < 0 ? UNBOUNDED : NUMERIC;
             st->slot[s].r = -1;
@@ -991,7 +997,7 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
             const int64_t grow = g.row0 + i;
             Cand c;
             c.theta = b > 0.0 ? b / a : 0.0;
-            c.piv = a;
+            c.piv = isfinite(b) ? a : __longlong_as_double(0x7ff8000000000000ll);   // b_r not finite: NUMERIC at prep
             c.row = grow;
             c.key = RULE == RULE_BLAND ? (grow == r ? kc : bkey) : grow;
             if (cand_better(c, best)) best = c;

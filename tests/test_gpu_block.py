@@ -196,3 +196,31 @@ def test_reload_into_a_solved_context(lpg, monkeypatch):
     ro2 = o2.solve(200_000, 0)
     assert r2.status == ro2.status == 1 and r2.objective == ro2.objective
     assert np.array_equal(e.get_rows(0, m + 1), o2.get_rows())
+
+
+@pytest.mark.parametrize("persist", [None, 0])
+@pytest.mark.parametrize("case", ["nan_b", "inf_b", "overflowing_ratio"])
+def test_numeric_rule_matches_oracle(lpg, monkeypatch, persist, case):
+    """The oracle stops NUMERIC when the chosen row's pivot element or b is not
+    finite (oracle/lpo.c lpo_solve) and otherwise pivots, an overflowing
+    ratio b / a included: the persistent kernel and the pair agree."""
+    m, n = 60, 90
+    o = Oracle(m, n + m + 1)
+    o.generate(n, 5, 0)
+    T = o.get_rows().copy()
+    basis = np.arange(n + 1, n + m + 1, dtype=np.int64)
+    if case == "nan_b":
+        T[7, 0] = np.nan
+    elif case == "inf_b":
+        T[7, 0] = -np.inf
+    else:                                      # b finite, b / a overflows for the entering column
+        T[7, 0] = 1e308
+        T[7, 1:n + 1] = 1e-10
+    o2 = Oracle(m, n + m + 1)
+    o2.load_tableau(T, basis)
+    ores = o2.solve(1000, 0)
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32, persist=persist)
+    e.load_tableau(T, basis)
+    res = e.solve(1000, 0)
+    assert res.status == ores.status and res.pivots == ores.pivots
+    assert _log(e) == _log(o2)
