@@ -71,9 +71,10 @@ constexpr int kRecR = 2;            // ratio record:   {theta, key, tag} {piv, r
 constexpr int kMaxLds = 150 * 1024;   // dynamic LDS cap (the slices)
 constexpr long long kSpinTicks = 200000000ll;   // s_memrealtime runs at 100 MHz: 2 s
 
-// doubles per thread row of the LDS slices: >= ks + 8 (a padded batch),
-// = 2 mod 4 (16-byte reads at this stride from 16 lanes cover the 64 banks)
-__host__ __device__ constexpr int slot_stride(int ks) { return ks + 8 + ((2 - (ks + 8) % 4) + 4) % 4; }
+// doubles per thread row of the LDS slices: the unrolled chains read 16, 32,
+// 48 or 64 slots, so >= ks rounded up to 16; = 2 mod 4 (16-byte reads at this
+// stride from 16 lanes cover the 64 banks once)
+__host__ __device__ constexpr int slot_stride(int ks) { return ((ks + 15) & ~15) + 2; }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, int bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, bytes, 0x00020000);

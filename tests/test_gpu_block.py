@@ -53,7 +53,7 @@ def _fits(m, ncols, defer, wg):
         return True
     ncp = (ncols + 1) & ~1
     cw, rw = -(-ncp // wg), -(-m // wg)
-    s = defer + 8 + ((2 - (defer + 8) % 4) + 4) % 4           # slot_stride
+    s = ((defer + 15) & ~15) + 2                           # slot_stride
     return cw <= 256 and rw <= 256 and s * (cw + rw) * 8 <= 150 * 1024
 
 
