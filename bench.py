@@ -6,9 +6,9 @@ the device (splitmix64, seed 20220518). Each simplex pivot is price (argmin
 over the reduced-cost row) -> ratio test (min over the entering column) ->
 Gauss-Jordan rank-1 update of the whole tableau. The update is deferred:
 prep / select evaluate the pending chain for the entries they need and
-k_flushw applies each block of K pivots (LPG_DEFER; 64 for tableaus >= 512 MB
-per rank, else 32) to the constraint rows in one HBM pass, bitwise identical
-to K eager updates.
+k_flushw applies each block of K pivots (LPG_DEFER; 128 for tableaus >= 16 GB
+per rank, 64 from 512 MB, else 32) to the constraint rows in one HBM pass,
+bitwise identical to K eager updates.
 
 A "step" is one such block: K pivots and the one pass over the tableau that
 applies them (with --defer 0, eager updates, a step is one pivot). `value` is

@@ -79,15 +79,17 @@ extern "C" {
 #define LPG_FLAG_EAGER   0x8u  /* one rank-1 update pass per pivot instead of deferred (blocked) updates */
 
 /* Deferred updates (default): the constraint rows are brought up to date in
- * one HBM pass per block of up to LPG_DEFER_MAX pivots (64 when a rank's
- * tableau is >= 512 MB, else 32; env LPG_DEFER=K picks K; 0 = eager). Values,
+ * one HBM pass per block of up to LPG_DEFER_MAX pivots (128 when a rank's
+ * tableau is >= 16 GB, 64 when >= 512 MB, else 32; env LPG_DEFER=K picks K,
+ * K in 1 .. 128; 0 = eager; the persistent pivot kernel takes blocks of at
+ * most 64). Values,
  * pivot sequence and log are bitwise those of eager updates; every call that
  * reads or replaces the tableau (lpg_get_rows, lpg_get_column0, lpg_load_rows,
  * lpg_set_basis, lpg_set_objective*, lpg_sync, lpg_device_sync, the end of
  * lpg_solve) applies the pending block first. Single-rank contexts may keep the
  * columns in a different physical order between such calls (nonbasic columns
  * contiguous); every call that exposes or takes columns sees caller order. */
-#define LPG_DEFER_MAX    64
+#define LPG_DEFER_MAX    128
 
 typedef struct lpg_ctx lpg_ctx;
 

@@ -24,7 +24,7 @@ FLAG_NO_LOG = 0x1
 FLAG_NO_SKIP = 0x2
 FLAG_BIG_M = 0x4
 FLAG_EAGER = 0x8
-DEFER_MAX = 64
+DEFER_MAX = 128
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int64_p = ctypes.POINTER(ctypes.c_int64)

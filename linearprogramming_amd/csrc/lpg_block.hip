@@ -668,6 +668,7 @@ int block_records_bytes(int nwg) { return nwg * (kRecPMax + kRecR) * 16; }
 // (config 2: 77.6k pivots/s on 256 workgroups, 99.8k on 16; config 5: 58.6k
 // on 256, 65.2k on 128; config 3 needs all 256 for the LDS).
 int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, int *rw, size_t *lds) {
+    if (ks < 1 || ks > 64) return -1;                      // blocks of <= 64 pivots (the slices' chains)
     const int64_t ncp = (g.ncols + 1) & ~(int64_t)1;
     const int64_t S = slot_stride(ks);
     const int64_t per_wg = kMaxLds / (S * (int64_t)sizeof(double));   // columns + rows one workgroup holds

@@ -28,7 +28,7 @@ namespace lpg {
 constexpr int kBlock = 256;          // threads per block everywhere (4 waves of 64)
 constexpr int kMaxSelBlocks = 512;   // ratio-test partials per rank
 #ifndef LPG_DEFER_MAX
-#define LPG_DEFER_MAX 64             // include/lpg.h
+#define LPG_DEFER_MAX 128            // include/lpg.h
 #endif
 
 enum : int32_t { RUNNING = 0, OPTIMAL = 1, UNBOUNDED = 2, INFEASIBLE = 3, ITER_LIMIT = 4, NUMERIC = 5 };

@@ -685,17 +685,25 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
         dR = *(const d2 *)(T + rR * g.ld + 2 * j2);
     }
     const double cM = -Cs[rM], cR = -Cs[rR];
-    const int npf = D.q < kPF ? D.q : kPF;
+    // kPF = 128: two banks of 64 slots (blocks of up to 128 pivots); bank 1
+    // holds slots 64 .. 127 in lanes 0 .. 63 and its P rows are loaded after
+    // bank 0's chain (the registers of a 128-row prefetch are not there: one
+    // more memory round trip, ~1 us, on pivots 65 .. 128 of a block)
+    constexpr int B0 = kPF < 64 ? kPF : 64;
+    constexpr bool TWO = kPF > 64;
+    static_assert(kPF <= 64 || kPF == 128, "prefetch slots");
+    const int npf = D.q < B0 ? D.q : B0;
     // slots past the block are (+0, +0) and their multiplier is -0: the chain
     // step fma(-0, +0, x) == x for every x, so the loop below needs no bound
     // (slots past the block load from an all-zero row: no branch and no
     // select per load, either of which makes the 64 loads wait in turn)
-    d2 pq[kPF];
+    d2 pq[B0];
     const int64_t jc = col ? 2 * j2 : 0;
 #pragma unroll
-    for (int u = 0; u < kPF; u++)
+    for (int u = 0; u < B0; u++)
         pq[u] = *(const d2 *)((u < npf ? D.Pbuf + (int64_t)u * g.ld : D.zrow) + jc);
     const int64_t rqv = lane < D.q ? D.rq[lane] : -1;   // lane q of every wave holds r_q
+    const int64_t rqv1 = TWO && 64 + lane < D.q ? D.rq[64 + lane] : -1;   // bank 1: r_{64 + lane}
     const int2 lj = col ? ((const int2 *)D.colmap)[j2] : int2{0, 0};   // logical indices of the two columns
     if (status != RUNNING) return;
     if (MODE == 2 && !X.from_cand && !xch_gather<NT>(X, best)) {
@@ -745,11 +753,15 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
     d2 t = d2{0.0, 0.0};
     if (col && own) t = *(const d2 *)(T + rl * g.ld + 2 * j2);
     const double cl = (own && lane < D.q) ? -D.Cbuf[(int64_t)lane * D.cs + rl] : -0.0;
+    const double cl1 = (TWO && own && 64 + lane < D.q) ? -D.Cbuf[(int64_t)(64 + lane) * D.cs + rl] : -0.0;
     const unsigned long long hit = __ballot(own && lane < D.q && rqv == rl);
-    const int qs = hit ? 63 - __clzll((long long)hit) : -1;
+    const unsigned long long hit1 = TWO ? __ballot(own && 64 + lane < D.q && rqv1 == rl) : 0ull;
+    const int qs = hit1 ? 127 - __clzll((long long)hit1) : hit ? 63 - __clzll((long long)hit) : -1;
     LPG_PH(0, 3);
     PricePart pbest{0.0, -1, 0, 0};
     const uint64_t clb = (uint64_t)__double_as_longlong(cl);
+    const uint64_t clb1 = (uint64_t)__double_as_longlong(cl1);
+    const int npf1 = TWO && D.q > 64 ? D.q - 64 : 0;
     // The chain runs in every lane (EXEC full, uniform branches only): a
     // readlane returns the source lane's register whether or not that lane
     // was active when the register was written, so the multipliers must never
@@ -758,28 +770,41 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
     // restart on this row.
     if (qs < 0) {
 #pragma unroll
-        for (int u = 0; u < kPF; u++) {
+        for (int u = 0; u < B0; u++) {
             const double c = __longlong_as_double((long long)rdl64(clb, u));
             t.x = fma(c, pq[u].x, t.x);
             t.y = fma(c, pq[u].y, t.y);
         }
     } else {
 #pragma unroll
-        for (int u = 0; u < kPF; u++) {
+        for (int u = 0; u < B0; u++) {
             const double c = __longlong_as_double((long long)rdl64(clb, u));
             const double fx = fma(c, pq[u].x, t.x), fy = fma(c, pq[u].y, t.y);
             t.x = u == qs ? pq[u].x : (u > qs ? fx : t.x);
             t.y = u == qs ? pq[u].y : (u > qs ? fy : t.y);
         }
     }
-    for (int q = kPF; q < D.q; q++) {       // blocks longer than kPF (the launcher avoids them)
-        const d2 v = col ? *(const d2 *)(D.Pbuf + (int64_t)q * g.ld + 2 * j2) : d2{0.0, 0.0};
-        const double c = __longlong_as_double((long long)rdl64(clb, q));
-        if (q == qs) {
-            t = v;
-        } else if (q > qs) {
-            t.x = fma(c, v.x, t.x);
-            t.y = fma(c, v.y, t.y);
+    if (TWO && D.q > 64) {                  // bank 1: slots 64 .. D.q - 1 (uniform)
+        asm volatile("" ::: "memory");      // its loads stay behind bank 0's chain
+#pragma unroll
+        for (int u = 0; u < 64; u++)
+            pq[u] = *(const d2 *)((u < npf1 ? D.Pbuf + (int64_t)(64 + u) * g.ld : D.zrow) + jc);
+        const int qs1 = qs - 64;
+        if (qs1 < 0) {
+#pragma unroll
+            for (int u = 0; u < 64; u++) {
+                const double c = __longlong_as_double((long long)rdl64(clb1, u));
+                t.x = fma(c, pq[u].x, t.x);
+                t.y = fma(c, pq[u].y, t.y);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 64; u++) {
+                const double c = __longlong_as_double((long long)rdl64(clb1, u));
+                const double fx = fma(c, pq[u].x, t.x), fy = fma(c, pq[u].y, t.y);
+                t.x = u == qs1 ? pq[u].x : (u > qs1 ? fx : t.x);
+                t.y = u == qs1 ? pq[u].y : (u > qs1 ? fy : t.y);
+            }
         }
     }
     if (MODE == 1) {
@@ -888,17 +913,32 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
         ob = T[i * g.ld];
         csi = Cs[i];
     }
-    const int npf = D.q < kPF ? D.q : kPF;
-    double cv[kPF];                  // slots past the pending block: +0 (with P entries +0 below: no-op steps)
+    // kPF = 128: two banks of 64 slots (blocks of up to 128 pivots; k_prep_d)
+    constexpr int B0 = kPF < 64 ? kPF : 64;
+    constexpr bool TWO = kPF > 64;
+    static_assert(kPF <= 64 || kPF == 128, "prefetch slots");
+    const int npf = D.q < B0 ? D.q : B0;
+    double cv[B0];                   // slots past the pending block: +0 (with P entries +0 below: no-op steps)
 #pragma unroll
-    for (int u = 0; u < kPF; u++) {
+    for (int u = 0; u < B0; u++) {
         cv[u] = 0.0;
         if (u < npf && crow) cv[u] = D.Cbuf[(int64_t)u * D.cs + i];
     }
-    // lane q of every wave holds P_q[0], r_q (q <= D.q: pivot t included)
+    double cv1[TWO ? 64 : 1];        // bank 1: slots 64 .. D.q - 1 (pivot t's own C_t is added below)
+    const int npf1 = TWO && D.q > 64 ? D.q - 64 : 0;
+#pragma unroll
+    for (int u = 0; u < (TWO ? 64 : 1); u++) {
+        cv1[u] = 0.0;
+        if (TWO && u < npf1 && crow) cv1[u] = D.Cbuf[(int64_t)(64 + u) * D.cs + i];
+    }
+    // lane q of every wave holds P_q[0], r_q (q <= D.q: pivot t included);
+    // bank 1 slot 64 + q in lane q
     const bool lq = lane <= D.q;
     const double p0l = lq ? D.Pbuf[(int64_t)lane * g.ld] : 0.0;
     const int32_t rql = lq ? (int32_t)D.rq[lane] : -1;
+    const bool lq1 = TWO && 64 + lane <= D.q;
+    const double p0l1 = lq1 ? D.Pbuf[(int64_t)(64 + lane) * g.ld] : 0.0;
+    const int32_t rql1 = lq1 ? (int32_t)D.rq[64 + lane] : -1;
     const int64_t bkey = (RULE == RULE_BLAND && crow) ? basis[g.row0 + i] : 0;
     Slot *dst = &st->slot[s1];
     if (stt != RUNNING) {
@@ -933,6 +973,7 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
     double oa = 0.0;
     if (row) oa = T[i * g.ld + kp];
     const double pkl = lq ? D.Pbuf[(int64_t)lane * g.ld + kp] : 0.0;
+    const double pkl1 = lq1 ? D.Pbuf[(int64_t)(64 + lane) * g.ld + kp] : 0.0;
     LPG_PH(1, 3);
     const uint64_t p0b = (uint64_t)__double_as_longlong(p0l), pkb = (uint64_t)__double_as_longlong(pkl);
     Cand best{0.0, 0.0, 0, -1};
@@ -943,14 +984,14 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
     // a per-lane condition
     double b = ob, a = oa;
     const int32_t ii = (int32_t)i;
-    if (D.q <= kPF) {
-        // straight line over kPF slots: lanes >= D.q read as (P = +0, r = -1)
+    if (D.q <= B0) {
+        // straight line over B0 slots: lanes >= D.q read as (P = +0, r = -1)
         // and cv = +0 there, so those steps are fma(-0, +0, x) == x
         const bool lp = lane < D.q;
         const uint64_t p0m = lp ? p0b : 0ull, pkm = lp ? pkb : 0ull;
         const uint32_t rqm = lp ? (uint32_t)rql : 0xffffffffu;
 #pragma unroll
-        for (int u = 0; u < kPF; u++) {
+        for (int u = 0; u < B0; u++) {
             const double q0 = __longlong_as_double((long long)rdl64(p0m, u));
             const double qk = __longlong_as_double((long long)rdl64(pkm, u));
             const bool hit = ii == (int32_t)rdl32(rqm, u);
@@ -960,7 +1001,7 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
         }
     } else {
 #pragma unroll
-        for (int u = 0; u < kPF; u++) {
+        for (int u = 0; u < B0; u++) {
             const double q0 = __longlong_as_double((long long)rdl64(p0b, u));
             const double qk = __longlong_as_double((long long)rdl64(pkb, u));
             const bool hit = ii == (int32_t)rdl32((uint32_t)rql, u);
@@ -969,16 +1010,23 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
             a = hit ? qk : fa;
         }
     }
-    for (int q = kPF; q <= D.q; q++) {   // the rest of a long block, and pivot t itself
-        const double q0 = __longlong_as_double((long long)rdl64(p0b, q));
-        const double qk = __longlong_as_double((long long)rdl64(pkb, q));
-        const double c = q == D.q ? -csi : (crow ? -D.Cbuf[(int64_t)q * D.cs + i] : -0.0);
-        const bool hit = ii == (int32_t)rdl32((uint32_t)rql, q);
-        const double fb = fma(c, q0, b), fa = fma(c, qk, a);
-        b = hit ? q0 : fb;
-        a = hit ? qk : fa;
+    if (TWO && D.q >= 64) {
+        // bank 1, pivot t included (slot D.q, multiplier -Cs): lanes past
+        // D.q - 64 read as (P = +0, r = -1) with multiplier +0
+        const uint64_t p0b1 = (uint64_t)__double_as_longlong(p0l1), pkb1 = (uint64_t)__double_as_longlong(pkl1);
+        const int qt = D.q - 64;
+#pragma unroll
+        for (int u = 0; u < 64; u++) {
+            const double q0 = __longlong_as_double((long long)rdl64(p0b1, u));
+            const double qk = __longlong_as_double((long long)rdl64(pkb1, u));
+            const bool hit = ii == (int32_t)rdl32((uint32_t)rql1, u);
+            const double c = u == qt ? csi : cv1[u];
+            const double fb = fma(-c, q0, b), fa = fma(-c, qk, a);
+            b = hit ? q0 : fb;
+            a = hit ? qk : fa;
+        }
     }
-    if (D.q < kPF) {          // pivot t itself: C_t is Cs
+    if (D.q < B0) {           // pivot t itself: C_t is Cs
         const int q = D.q;
         const double q0 = __longlong_as_double((long long)rdl64(p0b, q));
         const double qk = __longlong_as_double((long long)rdl64(pkb, q));
@@ -1033,6 +1081,11 @@ int debug_phases(unsigned long long *out, int reset) {
 }
 #endif
 
+// prefetch slots of k_prep_d / k_select_d: the pending chain rounded up to
+// 16 (padding slots cost a load and two fmas each, ~1.4 us per kernel for 32
+// of them), two banks of 64 past 64 pending pivots
+static int pivot_pf(int q) { return q < 16 ? 16 : q < 32 ? 32 : q < 48 ? 48 : q < 64 ? 64 : 128; }
+
 int pivot_d_blocks(const Geo &g, int which, int nt) {
     return which == 0 ? (int)(((g.ncols + 1) / 2 + nt - 1) / nt) : (int)((g.nloc + g.nobj + nt - 1) / nt);
 }
@@ -1058,19 +1111,19 @@ int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s,
     do {                                   \
         LPG_PD(R, PF, 256);                \
     } while (0)
-    // prefetch slots: the pending chain rounded up to 16 (padding slots cost
-    // a load and two fmas each, ~1.4 us per kernel for 32 of them)
-    const int pf = D.q < 16 ? 16 : D.q < 32 ? 32 : D.q < 48 ? 48 : 64;
+    const int pf = pivot_pf(D.q);
     if (rule == RULE_BLAND) {
         if (pf == 16) LPG_PD_NT(RULE_BLAND, 16);
         else if (pf == 32) LPG_PD_NT(RULE_BLAND, 32);
         else if (pf == 48) LPG_PD_NT(RULE_BLAND, 48);
-        else LPG_PD_NT(RULE_BLAND, 64);
+        else if (pf == 64) LPG_PD_NT(RULE_BLAND, 64);
+        else LPG_PD_NT(RULE_BLAND, 128);
     } else {
         if (pf == 16) LPG_PD_NT(RULE_DANTZIG, 16);
         else if (pf == 32) LPG_PD_NT(RULE_DANTZIG, 32);
         else if (pf == 48) LPG_PD_NT(RULE_DANTZIG, 48);
-        else LPG_PD_NT(RULE_DANTZIG, 64);
+        else if (pf == 64) LPG_PD_NT(RULE_DANTZIG, 64);
+        else LPG_PD_NT(RULE_DANTZIG, 128);
     }
 #undef LPG_PD_NT
 #undef LPG_PD
@@ -1087,17 +1140,19 @@ int launch_prep_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s,
 #define LPG_PM(R, PF)                                                                                                 \
     hipLaunchKernelGGL((k_prep_d<R, PF, 256, 1>), dim3(npp_d), dim3(256), 0, stream, g.T, g, st, s, cand, ncand, P,    \
                        Cs, nullptr, D, X0)
-    const int pf = D.q < 16 ? 16 : D.q < 32 ? 32 : D.q < 48 ? 48 : 64;   // as launch_pivot_d
+    const int pf = pivot_pf(D.q);   // as launch_pivot_d
     if (rule == RULE_BLAND) {
         if (pf == 16) LPG_PM(RULE_BLAND, 16);
         else if (pf == 32) LPG_PM(RULE_BLAND, 32);
         else if (pf == 48) LPG_PM(RULE_BLAND, 48);
-        else LPG_PM(RULE_BLAND, 64);
+        else if (pf == 64) LPG_PM(RULE_BLAND, 64);
+        else LPG_PM(RULE_BLAND, 128);
     } else {
         if (pf == 16) LPG_PM(RULE_DANTZIG, 16);
         else if (pf == 32) LPG_PM(RULE_DANTZIG, 32);
         else if (pf == 48) LPG_PM(RULE_DANTZIG, 48);
-        else LPG_PM(RULE_DANTZIG, 64);
+        else if (pf == 64) LPG_PM(RULE_DANTZIG, 64);
+        else LPG_PM(RULE_DANTZIG, 128);
     }
 #undef LPG_PM
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1114,17 +1169,19 @@ int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int 
 #define LPG_SM(R, PF)                                                                                               \
     hipLaunchKernelGGL((k_select_d<R, PF, 256, false>), dim3(nsel), dim3(256), 0, stream, g.T, g, st, s, s1, Cs, Cs1, \
                        pp, npp, basis, part, D, X0)
-    const int pf = D.q < 16 ? 16 : D.q < 32 ? 32 : D.q < 48 ? 48 : 64;   // as launch_pivot_d
+    const int pf = pivot_pf(D.q);   // as launch_pivot_d
     if (rule == RULE_BLAND) {
         if (pf == 16) LPG_SM(RULE_BLAND, 16);
         else if (pf == 32) LPG_SM(RULE_BLAND, 32);
         else if (pf == 48) LPG_SM(RULE_BLAND, 48);
-        else LPG_SM(RULE_BLAND, 64);
+        else if (pf == 64) LPG_SM(RULE_BLAND, 64);
+        else LPG_SM(RULE_BLAND, 128);
     } else {
         if (pf == 16) LPG_SM(RULE_DANTZIG, 16);
         else if (pf == 32) LPG_SM(RULE_DANTZIG, 32);
         else if (pf == 48) LPG_SM(RULE_DANTZIG, 48);
-        else LPG_SM(RULE_DANTZIG, 64);
+        else if (pf == 64) LPG_SM(RULE_DANTZIG, 64);
+        else LPG_SM(RULE_DANTZIG, 128);
     }
 #undef LPG_SM
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1146,17 +1203,19 @@ int launch_prep_x(const Launch &L, const Geo &g, int rule, DevState *st, int s, 
 #define LPG_PX(R, PF)                                                                                                 \
     hipLaunchKernelGGL((k_prep_d<R, PF, 256, 2>), dim3(npp_d), dim3(256), 0, stream, g.T, g, st, s, cand, ncand, P,    \
                        Cs, pp, D, X)
-    const int pf = D.q < 16 ? 16 : D.q < 32 ? 32 : D.q < 48 ? 48 : 64;   // as launch_pivot_d
+    const int pf = pivot_pf(D.q);   // as launch_pivot_d
     if (rule == RULE_BLAND) {
         if (pf == 16) LPG_PX(RULE_BLAND, 16);
         else if (pf == 32) LPG_PX(RULE_BLAND, 32);
         else if (pf == 48) LPG_PX(RULE_BLAND, 48);
-        else LPG_PX(RULE_BLAND, 64);
+        else if (pf == 64) LPG_PX(RULE_BLAND, 64);
+        else LPG_PX(RULE_BLAND, 128);
     } else {
         if (pf == 16) LPG_PX(RULE_DANTZIG, 16);
         else if (pf == 32) LPG_PX(RULE_DANTZIG, 32);
         else if (pf == 48) LPG_PX(RULE_DANTZIG, 48);
-        else LPG_PX(RULE_DANTZIG, 64);
+        else if (pf == 64) LPG_PX(RULE_DANTZIG, 64);
+        else LPG_PX(RULE_DANTZIG, 128);
     }
 #undef LPG_PX
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1170,17 +1229,19 @@ int launch_select_x(const Launch &L, const Geo &g, int rule, DevState *st, int s
 #define LPG_SX(R, PF)                                                                                              \
     hipLaunchKernelGGL((k_select_d<R, PF, 256, true>), dim3(nsel), dim3(256), 0, stream, g.T, g, st, s, s1, Cs, Cs1, \
                        pp, npp, basis, part, D, X)
-    const int pf = D.q < 16 ? 16 : D.q < 32 ? 32 : D.q < 48 ? 48 : 64;
+    const int pf = pivot_pf(D.q);
     if (rule == RULE_BLAND) {
         if (pf == 16) LPG_SX(RULE_BLAND, 16);
         else if (pf == 32) LPG_SX(RULE_BLAND, 32);
         else if (pf == 48) LPG_SX(RULE_BLAND, 48);
-        else LPG_SX(RULE_BLAND, 64);
+        else if (pf == 64) LPG_SX(RULE_BLAND, 64);
+        else LPG_SX(RULE_BLAND, 128);
     } else {
         if (pf == 16) LPG_SX(RULE_DANTZIG, 16);
         else if (pf == 32) LPG_SX(RULE_DANTZIG, 32);
         else if (pf == 48) LPG_SX(RULE_DANTZIG, 48);
-        else LPG_SX(RULE_DANTZIG, 64);
+        else if (pf == 64) LPG_SX(RULE_DANTZIG, 64);
+        else LPG_SX(RULE_DANTZIG, 128);
     }
 #undef LPG_SX
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1887,19 +1948,23 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T,
 // multipliers are staged in LDS once, so each P entry leaves HBM once (the
 // per-row form re-read P_u for every earlier pivot row: 98 us at config 3).
 // Each wave runs groups of 4 consecutive rows, so one LDS read of P_u[j]
-// feeds 4 chains (groups {w, 7-w, 8+w, 15-w}: equal work per wave); the
+// feeds 4 chains (groups {w, 7-w, 8+w, 15-w, ...}: equal work per wave); the
 // first steps of a group, where only some of its rows have started, are
-// peeled so that every row sees exactly its own steps.
+// peeled so that every row sees exactly its own steps. K = 64: the
+// multipliers are staged in LDS too; K = 128 (128 KB of them) reads them as
+// wave-uniform loads, and r_q of slots 64 .. 127 sits in a second register.
+template <int K>
 __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict__ T, Geo g,
                                                              const DevState *__restrict__ st,
                                                              const double *__restrict__ Pbuf,
                                                              const double *__restrict__ mul,
                                                              const int64_t *__restrict__ rq) {
-    constexpr int K = LPG_DEFER_MAX;
+    static_assert((K == 64 || K == 128) && K <= LPG_DEFER_MAX && kBlock == 256, "4 waves x K/16 groups of 4 rows");
+    constexpr bool LM = K == 64;                        // multipliers in LDS
     constexpr int PW = K / (kBlock / 64);               // P rows staged per wave
-    constexpr int MT = K * K / kBlock;                  // multipliers staged per thread
+    constexpr int MT = LM ? K * K / kBlock : 1;         // multipliers staged per thread
     __shared__ double sP[K][64];
-    __shared__ __attribute__((aligned(32))) double sM[K * K];   // [u][q]
+    __shared__ __attribute__((aligned(32))) double sM[LM ? K * K : 4];   // [u][q]
     const int np = (int)st->npend;
     if (np <= 0) return;
     const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1914,24 +1979,28 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
         }
 #pragma unroll
         for (int k = 0; k < MT; k++) {
-            const int e = threadIdx.x + kBlock * k;
-            m[k] = (e >> 6) < np ? mul[e] : 0.0;
+            const int e = threadIdx.x + kBlock * k;   // [u][q] in rows of K
+            m[k] = (LM && e / K < np) ? mul[(e / K) * LPG_DEFER_MAX + e % K] : 0.0;
         }
 #pragma unroll
         for (int k = 0; k < PW; k++) sP[w + 4 * k][c] = v[k];
+        if (LM) {
 #pragma unroll
-        for (int k = 0; k < MT; k++) sM[threadIdx.x + kBlock * k] = m[k];
+            for (int k = 0; k < MT; k++) sM[threadIdx.x + kBlock * k] = m[k];
+        }
     }
     const int64_t ru = c < np ? rq[c] : -1;             // lane u: r_u
+    const int64_t ru1 = K > 64 && 64 + c < np ? rq[64 + c] : -1;   // lane u: r_{64 + u}
     __syncthreads();
-    static_assert(K == 64 && kBlock == 256, "4 waves x 4 groups of 4 rows");
 #pragma unroll 1
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < K / 16; k++) {
         const int grp = (k & 1) ? 8 * (k >> 1) + 7 - w : 8 * (k >> 1) + w;
         const int q0 = 4 * grp;
         if (q0 >= np) continue;                         // uniform
         double x0 = sP[q0][c], x1 = sP[q0 + 1][c], x2 = sP[q0 + 2][c], x3 = sP[q0 + 3][c];
-        auto m4 = [&](int u) { return *(const d4 *)(sM + u * K + q0); };   // mul[u][q0 .. q0 + 3]
+        auto m4 = [&](int u) {                          // mul[u][q0 .. q0 + 3]
+            return LM ? *(const d4 *)(sM + u * K + q0) : *(const d4 *)(mul + u * LPG_DEFER_MAX + q0);
+        };
         if (q0 + 1 < np) {
             const double p = sP[q0 + 1][c];
             const d4 m = m4(q0 + 1);
@@ -1964,9 +2033,10 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
         for (int i = 0; i < 4; i++) {
             const int q = q0 + i;
             if (q >= np) break;                         // uniform
-            const int64_t r = (int64_t)rdl64((uint64_t)ru, q);
+            const int64_t r = q < 64 ? (int64_t)rdl64((uint64_t)ru, q) : (int64_t)rdl64((uint64_t)ru1, q - 64);
             if (r < 0) continue;                        // pivot row on another rank
             if (__ballot(c > q && ru == r)) continue;   // a later pivot replaces this row again
+            if (K > 64 && __ballot(64 + c > q && ru1 == r)) continue;
             if (ok) T[r * g.ld + j] = xs[i];
         }
     }
@@ -1999,7 +2069,8 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
 // plan != 0). Blocks 1..: the multipliers of k_flush_pivot_rows,
 // mul[u][q] = -C_u[r_q] for u > q (+0 elsewhere), rows of LPG_DEFER_MAX.
 constexpr int kMulBlocks = 8;
-__global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ st, const int64_t *__restrict__ kq,
+constexpr int kPlanNT = LPG_DEFER_MAX;                     // one thread per event / slot
+__global__ __launch_bounds__(kPlanNT) void k_swap_plan(const DevState *__restrict__ st, const int64_t *__restrict__ kq,
                                                   const int64_t *__restrict__ lv, const int64_t *__restrict__ rq,
                                                   const double *__restrict__ Cbuf, int64_t cs,
                                                   int32_t *__restrict__ colmap, int32_t *__restrict__ inv,
@@ -2028,13 +2099,17 @@ __global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ s
     // pivot element of pivot q (C_q[r_q], recorded by k_prep_d on every rank, so that every rank of a
     // row partition -- most of which do not hold row r_q -- makes the same plan)
     const bool pos = q >= np || pv[q] > 0.0;
+    __shared__ int64_t sx[kPlanNT], sy[kPlanNT];          // the events, read back as broadcasts
+    sx[q] = x;
+    sy[q] = y;
     // x (entering at q) is in E iff no later event touches x and its first event is an entry
     bool inE = q < np, inL = q < np;
     int fx = q, fy = q;           // first event index of x / y, and its kind
     bool fxe = true, fye = false;
+    const bool allpos = __syncthreads_count(!pos) == 0;   // also publishes sx / sy
+#pragma unroll 8
     for (int u = 0; u < np; u++) {
-        // event u from lane u (x, y computed with EXEC full)
-        const int64_t a = (int64_t)rdl64((uint64_t)x, u), b = (int64_t)rdl64((uint64_t)y, u);
+        const int64_t a = sx[u], b = sy[u];
         if (u > q) {
             if (a == x || b == x) inE = false;
             if (a == y || b == y) inL = false;
@@ -2045,20 +2120,34 @@ __global__ __launch_bounds__(64) void k_swap_plan(const DevState *__restrict__ s
             if (b == y && u < fy) { fy = u; fye = false; }
         }
     }
-    const bool allpos = __ballot(!pos) == 0ull;
     inE = inE && fxe && allpos;
     inL = inL && !fye && allpos;
+    // ranks in event order: within the wave by ballot, across waves by the counts of the waves before
+    constexpr int NW = kPlanNT / 64;
+    const int lane = q & 63, wv = q >> 6;
     const unsigned long long me = __ballot(inE), ml = __ballot(inL);
-    const unsigned long long below = (q == 0) ? 0ull : (~0ull >> (64 - q));
-    const int ie = __popcll(me & below), il = __popcll(ml & below);
-    __shared__ int64_t eE[64], eL[64], eR[64];
+    __shared__ int cE[NW], cL[NW];
+    if (lane == 0) {
+        cE[wv] = __popcll(me);
+        cL[wv] = __popcll(ml);
+    }
+    __syncthreads();
+    int oE = 0, oL = 0, n = 0;   // n: |E| == |L|
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        oE += w < wv ? cE[w] : 0;
+        oL += w < wv ? cL[w] : 0;
+        n += cE[w];
+    }
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int ie = oE + __popcll(me & below), il = oL + __popcll(ml & below);
+    __shared__ int64_t eE[kPlanNT], eL[kPlanNT], eR[kPlanNT];
     if (inE) {
         eE[ie] = x;
         eR[ie] = rx;
     }
     if (inL) eL[il] = y;
     __syncthreads();
-    const int n = __popcll(me);   // == __popcll(ml)
     if (q < n) {
         const int64_t ce = eE[q], cl = eL[q];
         const int32_t a = inv[ce], b = inv[cl];
@@ -2130,7 +2219,7 @@ __global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Ge
 
 int launch_swap_plan(const Launch &L, const DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
                      int32_t *pairs, int plan) {
-    hipLaunchKernelGGL(k_swap_plan, dim3(1 + kMulBlocks), dim3(64), 0, (hipStream_t)L.stream, st, D.kq, D.lv, D.rq,
+    hipLaunchKernelGGL(k_swap_plan, dim3(1 + kMulBlocks), dim3(kPlanNT), 0, (hipStream_t)L.stream, st, D.kq, D.lv, D.rq,
                        D.Cbuf, D.cs, colmap, inv, pairs, D.mul, plan, D.pv);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -2182,6 +2271,7 @@ int flush_kmax_supported(int k) {
     if (k <= 16) return 16;
     if (k <= 32) return 32;
     if (k <= 64) return 64;
+    if (k <= 128 && k <= LPG_DEFER_MAX) return 128;
     return 0;
 }
 
@@ -2193,8 +2283,12 @@ int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &
     if (!kmax) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
     const int64_t ntiles_p = (g.ncols + 63) / 64;   // k_flush_pivot_rows column tiles
-    hipLaunchKernelGGL(k_flush_pivot_rows, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st, D.Pbuf, D.mul,
-                       D.rq);
+    if (kmax > 64)
+        hipLaunchKernelGGL(k_flush_pivot_rows<128>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
+                           D.Pbuf, D.mul, D.rq);
+    else
+        hipLaunchKernelGGL(k_flush_pivot_rows<64>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
+                           D.Pbuf, D.mul, D.rq);
     if (hipGetLastError() != hipSuccess) return -1;
     // the pending block is applied: clear it and the dequeue head
     return hipMemsetAsync(&st->npend, 0, sizeof(int64_t) + sizeof(unsigned long long), stream) == hipSuccess ? 0 : -1;
@@ -2211,21 +2305,26 @@ int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, in
 int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which) {
     kmax = flush_kmax_supported(kmax);
     if (!kmax) return -1;
-    if (which < 0) which = kmax == 64 ? 1 : 0;
-    if (kmax == 64) which = 1;                              // k_flushm's C tile caps it at 32 slots
+    if (which < 0) which = kmax >= 64 ? 1 : 0;
+    if (kmax >= 64) which = 1;                              // k_flushm's C tile caps it at 32 slots
     hipStream_t stream = (hipStream_t)L.stream;
     if (which == 1) {
         // k_flushw: 4-wave blocks, 128-column x 512-row items swept in 16-row
         // bands with a 2-deep LDS ring of multipliers; small tableaus shrink
         // the items until they fill the chip
         const int64_t ntiles = (g.ncols + 127) / 128;
+        // (taller items measured at config 4: 1024 / 2048 rows within 1% of 512;
+        // 128 rows 13% slower)
         int64_t rows = 512;
         while (rows > 64 && ntiles * ((g.nloc + rows - 1) / rows) < 2048) rows /= 2;
         const int64_t nitems = ntiles * ((g.nloc + rows - 1) / rows);
-        const int lb = kmax == 64 ? 2 : 3;                  // VGPRs: 184 at 64 slots, <= 128 below
+        const int lb = kmax == 128 ? 1 : kmax == 64 ? 2 : 3;   // VGPRs: 184 at 64 slots, <= 128 below
         const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * lb);
         if (nblocks < 1) return 0;
-        if (kmax == 64)
+        if (kmax == 128)
+            hipLaunchKernelGGL((k_flushw<128, 2, 1, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
+                               D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
+        else if (kmax == 64)
             hipLaunchKernelGGL((k_flushw<64, 2, 2, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
                                D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
         else

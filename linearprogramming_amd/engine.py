@@ -57,8 +57,8 @@ def _stdout_to_stderr():
 
 def flush_kernel_for(pending: int) -> str:
     """Which block-pass kernel the default configuration launches for `pending`
-    pivots (lpg_kernels.hip launch_flush_main): "w" = k_flushw (a 64-slot
-    block), "m" = k_flushm (<= 32 slots)."""
+    pivots (lpg_kernels.hip launch_flush_main): "w" = k_flushw (64- and
+    128-slot blocks), "m" = k_flushm (<= 32 slots)."""
     return "w" if pending > 32 else "m"
 
 

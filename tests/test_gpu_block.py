@@ -68,6 +68,7 @@ def test_engaged_where_the_slices_fit(lpg, monkeypatch):
     assert e.info.pivot_wg > 0
     assert _engine(lpg, monkeypatch, 600, 1701, defer=32, persist=0).info.pivot_wg == 0
     assert _engine(lpg, monkeypatch, 600, 1701, defer=0).info.pivot_wg == 0      # eager updates
+    assert _engine(lpg, monkeypatch, 600, 1701, defer=65).info.pivot_wg == 0     # blocks of > 64 pivots: the pair
     # 256 workgroups hold at most 256 columns each: wider tableaus keep the pair
     assert _engine(lpg, monkeypatch, 8, 256 * 256 + 3, defer=8).info.pivot_wg == 0
 

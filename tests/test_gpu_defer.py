@@ -44,7 +44,7 @@ def _engine(lpg, monkeypatch, k, m, ncols, **kw):
     return e
 
 
-@pytest.mark.parametrize("k", [0, 1, 2, 3, 8, 16, 31, 32, 64])
+@pytest.mark.parametrize("k", [0, 1, 2, 3, 8, 16, 31, 32, 64, 65, 100, 128])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(200, 300, 12, 0, 0), (48, 48, 14, 1, 1), (257, 100, 15, 1, 0)])
 def test_block_sizes_to_optimality(lpg, monkeypatch, k, m, n, seed, kind, rule):
     e = _engine(lpg, monkeypatch, k, m, n + m + 1)
@@ -58,7 +58,7 @@ def test_block_sizes_to_optimality(lpg, monkeypatch, k, m, n, seed, kind, rule):
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("k", [8, 32, 64])
+@pytest.mark.parametrize("k", [8, 32, 64, 128])
 def test_config2_to_optimality(lpg, monkeypatch, k):
     m, n = 1024, 2048
     e = _engine(lpg, monkeypatch, k, m, n + m + 1)
@@ -71,15 +71,16 @@ def test_config2_to_optimality(lpg, monkeypatch, k):
     _assert_same(e, o, m)
 
 
-def test_reads_inside_a_block(lpg, monkeypatch):
+@pytest.mark.parametrize("k", [32, 128])
+def test_reads_inside_a_block(lpg, monkeypatch, k):
     """Reads in the middle of a block flush it; the loop then continues from the
     flushed tableau and stays on the oracle's path."""
     m, n = 150, 220
-    e = _engine(lpg, monkeypatch, 32, m, n + m + 1)
+    e = _engine(lpg, monkeypatch, k, m, n + m + 1)
     o = Oracle(m, n + m + 1)
     e.generate(n, 71, 0)
     o.generate(n, 71, 0)
-    for step in (5, 1, 13, 32, 40, 3):
+    for step in (5, 1, 13, 32, 40, 3, 70, 90):
         e.enqueue(step, 0)
         assert e.get_column0().shape == (m,)           # flushes
         o.solve(step, 0)
@@ -104,7 +105,7 @@ def test_enqueue_past_optimal_partial_block(lpg, monkeypatch):
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("kernel,k", [("m", 8), ("m", 16), ("m", 32), ("w", 8), ("w", 32), ("w", 64)])
+@pytest.mark.parametrize("kernel,k", [("m", 8), ("m", 16), ("m", 32), ("w", 8), ("w", 32), ("w", 64), ("w", 128)])
 def test_flush_kernels_identical(lpg, monkeypatch, kernel, k):
     """k_flushm and k_flushw at their block sizes (LPG_FLUSH_KERNEL forces one)."""
     monkeypatch.setenv("LPG_FLUSH_KERNEL", kernel)
@@ -146,12 +147,12 @@ def test_eager_flag(lpg):
 
 
 def test_bad_block_size(lpg, monkeypatch):
-    monkeypatch.setenv("LPG_DEFER", "65")
+    monkeypatch.setenv("LPG_DEFER", "129")
     with pytest.raises(lpg.LPGError):
         lpg.Engine(8, 20)
 
 
-@pytest.mark.parametrize("kernel,k", [("m", 3), ("m", 8), ("m", 32), ("w", 3), ("w", 32), ("w", 64)])
+@pytest.mark.parametrize("kernel,k", [("m", 3), ("m", 8), ("m", 32), ("w", 3), ("w", 32), ("w", 64), ("w", 77), ("w", 128)])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1)])
 def test_flush_kernels_block_sizes(lpg, monkeypatch, kernel, k, m, n, seed, kind, rule):
     """k_flushm (strip-staged C) and k_flushw (tall banded items) at every
@@ -168,7 +169,7 @@ def test_flush_kernels_block_sizes(lpg, monkeypatch, kernel, k, m, n, seed, kind
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("k", [5, 32, 40, 64])
+@pytest.mark.parametrize("k", [5, 32, 40, 64, 96, 128])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1)])
 def test_generic_and_prefetching_pivot_kernels_agree(lpg, monkeypatch, k, m, n, seed, kind, rule):
     """The deferred single-rank pivot runs through k_prep_d / k_select_d; the generic
@@ -187,7 +188,7 @@ def test_generic_and_prefetching_pivot_kernels_agree(lpg, monkeypatch, k, m, n, 
     _assert_same(f, o, m)
 
 
-@pytest.mark.parametrize("k", [32, 64])
+@pytest.mark.parametrize("k", [32, 64, 128])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1), (600, 1100, 3, 0, 0)])
 def test_reordered_columns_to_optimality(lpg, monkeypatch, k, m, n, seed, kind, rule):
     """Whole solves over many blocks: after every block the columns are reordered
@@ -204,7 +205,7 @@ def test_reordered_columns_to_optimality(lpg, monkeypatch, k, m, n, seed, kind, 
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("k", [32, 64])
+@pytest.mark.parametrize("k", [32, 64, 128])
 @pytest.mark.parametrize("rule,cap", [(0, 200_000), (1, 3000)])
 def test_wide_tableau_more_partials_than_threads(lpg, monkeypatch, k, rule, cap):
     """ncols > 131072: k_prep_d leaves more pricing partials (two columns per

@@ -90,11 +90,11 @@ def lpg():
     return lpg
 
 
-@pytest.mark.parametrize("defer", [None, "0", "5", "64"])
+@pytest.mark.parametrize("defer", [None, "0", "5", "64", "128"])
 @pytest.mark.parametrize("world,m,n,kind,rule", [(2, 96, 160, 0, 0), (3, 101, 77, 0, 0), (2, 64, 64, 1, 1),
                                                  (4, 203, 301, 0, 0), (8, 203, 301, 0, 0)])
 def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule, defer, monkeypatch):
-    """Row blocks over ranks; default deferred blocks, eager (0), 5- and 64-pivot blocks."""
+    """Row blocks over ranks; default deferred blocks, eager (0), 5-, 64- and 128-pivot blocks."""
     if defer is not None:
         monkeypatch.setenv("LPG_DEFER", defer)
     seed = 777
@@ -175,7 +175,7 @@ def test_two_processes_gloo_bitwise(lpg):
 
 @pytest.mark.parametrize("world,m,n,kind,rule,defer", [(2, 120, 200, 0, 0, None), (2, 96, 160, 0, 0, "5"),
                                                        (3, 101, 77, 0, 0, "64"), (2, 64, 64, 1, 1, "5"),
-                                                       (3, 203, 301, 0, 0, "32")])
+                                                       (3, 203, 301, 0, 0, "32"), (2, 203, 301, 0, 0, "128")])
 def test_processes_owner_push_bitwise(lpg, world, m, n, kind, rule, defer):
     """The owner-push exchange between ranks in separate processes sharing the
     GPU (IPC-mapped exchange buffers, the layout of one process per GPU): no
@@ -188,7 +188,7 @@ def test_processes_owner_push_bitwise(lpg, world, m, n, kind, rule, defer):
 
 
 @pytest.mark.parametrize("m,n,defer,graphs", [(300, 500, None, "0"), (1024, 2048, None, "0"), (1024, 2048, "64", "0"),
-                                              (1024, 2048, None, "1")])
+                                              (1024, 2048, "128", "0"), (1024, 2048, None, "1")])
 def test_rccl_single_rank_communicator(lpg, m, n, defer, graphs, monkeypatch):
     """The RCCL transport on a 1-rank communicator: every per-pivot ncclAllReduce
     (pivot row) and ncclAllGather (ratio candidates) really runs, and the result

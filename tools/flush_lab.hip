@@ -15,7 +15,10 @@
 // 2.93 ms = 47 TFLOP/s of the 75 the f64 MFMA pipe reaches: at 128 slots the
 // operands no longer fit beside a prefetch set, the compiler serialises each
 // LDS read of B behind the MFMAs that consume the previous one, and 1 wave
-// per SIMD cannot hide it.
+// per SIMD cannot hide it. Two 16-row bands per step in k_flushw<128> (4
+// independent MFMA chains per wave instead of 2) is no faster either: 3.07 ms
+// (profiles/r02_flush_lab_k128_sb2.log), so the 1-wave issue stream, not the
+// chain latency, is the limit.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o tools/flush_lab tools/flush_lab.hip
 //   tools/flush_lab [rows]            (LAB_ONLY=substring picks designs)
 #include "../linearprogramming_amd/csrc/lpg_kernels.hip"
