@@ -9,13 +9,13 @@
 * config 5 (two-phase, Bland, m = n = 8192, KM-style degenerate with
   equality rows): the whole solve to optimality, bitwise against the oracle
   (status, pivot count, objective, log, basis, sampled rows).
-* config 4 (65536 x 131072, 103 GB tableau, one GPU): 192 pivots (three
-  blocks); the oracle cannot hold it, so size-independent properties over the
+* config 4 (65536 x 131072, 103 GB tableau, one GPU): 320 pivots (two
+  whole 128-pivot blocks, then a partial one of 64); the oracle cannot hold it, so size-independent properties over the
   WHOLE tableau, read back in row chunks: every basic column is a unit vector
   in every row, b >= 0 (primal feasibility), z is nondecreasing block to block,
   and the objective row equals c_B T - c (recomputed on the host in global row
   order on ~64 sampled columns and on column 0) to 1e-9 relative to
-  sum |c_B| |T| -- the device row is the result of 192 rank-1 updates, not of
+  sum |c_B| |T| -- the device row is the result of 320 rank-1 updates, not of
   that dot product, so this one is a tolerance, not bitwise.
 
 Reference: the pivot loop simplex.c:40 -> :65 lacks.
@@ -108,17 +108,17 @@ def test_config4_full_size_properties(lpg):
     m, n = 65536, 131072
     N1 = n + m + 1
     e = lpg.Engine(m, N1)
-    assert e.info.defer_k == 64
+    assert e.info.defer_k == 128                 # >= 16 GB: 128-pivot blocks
     e.generate(n, SEED, lpg.GEN_DENSE)
     c = -e.get_rows(m, 1)[0, 1:]                # slack basis: row m = [0 | -c]
     assert np.all(c[:n] > 0) and np.all(c[n:] == 0)
-    e.reserve_log(256)
+    e.reserve_log(512)
     zs = [0.0]
-    for _ in range(3):
-        r = e.solve(64, lpg.RULE_DANTZIG)
+    for step in (128, 128, 64):
+        r = e.solve(step, lpg.RULE_DANTZIG)
         assert r.status_name == "ITER_LIMIT"
         zs.append(r.objective)
-    assert r.pivots == 192
+    assert r.pivots == 320
     assert all(b >= a for a, b in zip(zs, zs[1:])) and zs[-1] > 0
     basis = e.get_basis()
     assert len(set(basis.tolist())) == m
