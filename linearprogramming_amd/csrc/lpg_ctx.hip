@@ -326,10 +326,10 @@ static int flush_launch(lpg_ctx *c) {
     if (launch_flush_main(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, c->skip, c->flush_variant))
         return fail(c, LPG_ERR_DEVICE, "flush launch failed");
     if (c->timing && (rc = timing_mark(c, 2, 2))) return rc;
-    if (launch_flush_tail(lau(c), geo(c), c->st, defer_of(c, 0), c->pend))
+    if (launch_flush_tail(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, !re))
         return fail(c, LPG_ERR_DEVICE, "flush launch failed");
-    if (re) {
-        if (launch_fill_cols(lau(c), geo(c), c->pairs)) return fail(c, LPG_ERR_DEVICE, "fill launch failed");
+    if (re) {   // k_fill_cols also clears the pending block
+        if (launch_fill_cols(lau(c), geo(c), c->pairs, c->st)) return fail(c, LPG_ERR_DEVICE, "fill launch failed");
         c->permuted = true;
     }
     c->pend = 0;

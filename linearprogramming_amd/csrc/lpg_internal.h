@@ -185,7 +185,8 @@ int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, in
 // the pivot-row rewrite and the pending-counter reset (the rewrite's
 // multipliers come from launch_swap_plan, launched before either part)
 int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which);
-int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax);
+// reset = false: the caller clears npend / fwork itself (launch_fill_cols with st)
+int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, bool reset = true);
 int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0: k too large)
 // Basis-partitioned column order (single-rank deferred path): after a block,
 // every column that went nonbasic -> basic during it swaps its physical
@@ -201,7 +202,9 @@ int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0:
 int launch_swap_plan(const Launch &L, const DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
                      int32_t *pairs, int plan);   // reads D.pv (replicated pivot elements)
 int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs);
-int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs);
+// st != nullptr: also clears the pending block (npend, fwork), in place of
+// launch_flush_tail's memset (one dispatch fewer per block)
+int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs, DevState *st = nullptr);
 // Canonical order again: rows [i0, i0 + nr) gathered through inv into tmp
 // (nr x ld), then copied back; launch_iota resets colmap / inv.
 int launch_gather_rows(const Launch &L, const Geo &g, const int32_t *inv, double *tmp, int64_t i0, int64_t nr);

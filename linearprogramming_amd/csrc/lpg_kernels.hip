@@ -2207,8 +2207,15 @@ __global__ __launch_bounds__(kBlock) void k_move_cols(double *__restrict__ T, Ge
     }
 }
 
-// grid: (row blocks, 4): constraint row i, pairs p = blockIdx.y (mod 4)
-__global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Geo g, const int32_t *__restrict__ pairs) {
+// grid: (row blocks, 4): constraint row i, pairs p = blockIdx.y (mod 4).
+// st: the pending block is applied, clear it and the dequeue head (no kernel
+// of this launch reads them)
+__global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Geo g, const int32_t *__restrict__ pairs,
+                                                      DevState *__restrict__ st) {
+    if (st && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        st->npend = 0;
+        st->fwork = 0;
+    }
     const int n = pairs[0];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= g.nloc || n == 0) return;
@@ -2231,9 +2238,9 @@ int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const De
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs) {
-    hipLaunchKernelGGL(k_fill_cols, dim3((unsigned)((g.nloc + kBlock - 1) / kBlock), 4), dim3(kBlock), 0,
-                       (hipStream_t)L.stream, g.T, g, pairs);
+int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs, DevState *st) {
+    hipLaunchKernelGGL(k_fill_cols, dim3((unsigned)std::max<int64_t>((g.nloc + kBlock - 1) / kBlock, 1), 4), dim3(kBlock),
+                       0, (hipStream_t)L.stream, g.T, g, pairs, st);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2278,7 +2285,7 @@ int flush_kmax_supported(int k) {
 static_assert(offsetof(DevState, fwork) == offsetof(DevState, npend) + sizeof(int64_t),
               "launch_flush clears npend and fwork with one memset");
 
-int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax) {
+int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, bool reset) {
     kmax = flush_kmax_supported(kmax);
     if (!kmax) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
@@ -2290,6 +2297,7 @@ int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &
         hipLaunchKernelGGL(k_flush_pivot_rows<64>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
                            D.Pbuf, D.mul, D.rq);
     if (hipGetLastError() != hipSuccess) return -1;
+    if (!reset) return 0;
     // the pending block is applied: clear it and the dequeue head
     return hipMemsetAsync(&st->npend, 0, sizeof(int64_t) + sizeof(unsigned long long), stream) == hipSuccess ? 0 : -1;
 }
