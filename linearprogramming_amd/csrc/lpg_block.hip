@@ -196,10 +196,68 @@ __device__ __forceinline__ void rec_min(const u4 (&rec)[kPer][NG], int nwg, uint
 struct Bcast {            // one phase's decision, from wave 0 to the workgroup
     uint64_t h;
     uint32_t l;
-    int32_t ok;           // 1: decided, 0: none (OPTIMAL / UNBOUNDED), -1: timeout
+    int32_t ok;           // 1: decided, 0: none (OPTIMAL / UNBOUNDED), -1: timeout, -2: exchange timeout
     uint64_t p0, p1, p2, p3;   // winner payload
     uint64_t z;           // P_q[0]
 };
+
+// Multi-rank (owner-push exchange, Xch, lpg_internal.h). Workgroup 0 of every
+// rank stores its rank's best ratio candidate {theta bits, key, piv bits,
+// row} as 6 self-validating 8-byte words {payload, tag} into slot 0 of its
+// rank in every rank's xC (system-scope stores; lane 0 only) ...
+__device__ __forceinline__ void xpush_best(const Xch &X, uint32_t tag, uint64_t h, uint32_t l, uint64_t p0,
+                                           uint64_t p1) {
+    const uint32_t w[6] = {(uint32_t)h, (uint32_t)(h >> 32), (uint32_t)p0, (uint32_t)(p0 >> 32), l, (uint32_t)p1};
+    for (int rk = 0; rk < X.world; rk++) {
+        uint64_t *d = xch_cand(X, rk, tag & 1, X.rank, 0);
+#pragma unroll
+        for (int k = 0; k < 6; k++) st_sys64(d + k, ((uint64_t)tag << 32) | w[k]);
+    }
+}
+// ... and wave 0 of every workgroup polls its own xC (lane l: rank l) until
+// every rank's words carry the tag, then takes the lexicographic min. False
+// on timeout.
+__device__ bool xpoll_best(const Xch &X, uint32_t tag, uint64_t &h, uint32_t &l, uint64_t &p0, uint64_t &p1,
+                           DevState *st) {
+    const int lane = threadIdx.x & 63;
+    const long long t0 = (long long)wall_clock64();
+    uint64_t v[6] = {0, 0, 0, 0, 0, 0};
+    for (;;) {
+        bool ok = true;
+        if (lane < X.world) {
+            const uint64_t *w = xch_cand(X, X.rank, tag & 1, lane, 0);
+#pragma unroll
+            for (int k = 0; k < 6; k++) v[k] = ld_sys64(w + k);
+#pragma unroll
+            for (int k = 0; k < 6; k++) ok = ok && (uint32_t)(v[k] >> 32) == tag;
+        }
+        if (__all(ok)) break;
+        if ((long long)wall_clock64() - t0 > kSpinTicks) {
+            if (lane == 0) {
+                st->stall_info[0] = 4;
+                st->stall_info[1] = tag;
+            }
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    const uint64_t lo = 0xffffffffull;
+    uint64_t mh = ~0ull, m0 = 0, m1 = 0;
+    uint32_t ml = ~0u;
+    if (lane < X.world) {
+        mh = (v[0] & lo) | ((v[1] & lo) << 32);
+        m0 = (v[2] & lo) | ((v[3] & lo) << 32);
+        ml = (uint32_t)v[4];
+        m1 = v[5] & lo;
+    }
+    h = mh;
+    l = ml;
+    wave_min_key(h, l);
+    const int wl = winner_lane(lane < X.world && mh == h && ml == l);
+    p0 = wl < 0 ? 0 : rdl64(m0, wl);
+    p1 = wl < 0 ? 0 : rdl64(m1, wl);
+    return true;
+}
 
 }  // namespace
 
@@ -284,8 +342,12 @@ struct BlockArgs {
     Geo g;
     DevState *st;
     int s0, q0, n;               // parity and pending index of the first pivot; pivots in this launch
-    Cand *part;                  // in: ncand ratio candidates; out: one per workgroup, none up to ncand
+    Cand *part;                  // out: one ratio candidate per workgroup, none up to ncand
     int ncand;
+    const Cand *cin;             // in: the first pivot's ratio candidates (ncin; == part on one rank)
+    int ncin;
+    Xch X;                       // multi-rank: the owner-push exchange
+    uint32_t xtag0;              // multi-rank: exchange tag of pivot i of this launch = xtag0 + i
     const double *Cs0;           // C[s0]: the first pivot's column snapshot (incl. objective rows)
     double *Cs1;                 // C[(s0 + n) & 1]: the snapshot the launch leaves behind
     Defer D;
@@ -294,12 +356,21 @@ struct BlockArgs {
     int nwg, cw, rw, ks;         // workgroups, columns / rows per slice, LDS slots
 };
 
-template <int RULE, int NOBJ>
+// MR (multi-rank, row partition; Xch attached): the leaving row is the
+// minimum over every rank's best ratio candidate (xpush_best / xpoll_best);
+// the owner of row r computes the pivot row on each slice and stores it into
+// every other rank's xP behind a per-workgroup flag, the other ranks'
+// workgroups wait for their slice's flag and read it. Pricing needs no
+// exchange: P and the objective rows are replicated, so every rank takes the
+// same entering column from its own records. rq holds LOCAL rows (-1: another
+// rank's), the replicated basis / lv are kept by workgroup 0 of every rank.
+template <int RULE, int NOBJ, bool MR>
 __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     // pricing record granules: {key, j} {dR, phys} {P_q[phys]} {P_q[0] (workgroup 0)} [{dM}]
     constexpr int NGP = NOBJ == 2 ? 5 : 4;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ Bcast bc;
+    __shared__ int xok;
     // per wave, by pending slot: the pivot row's multipliers -C_u[r] (phase P)
     // and the entering column's P_u[k] (phase S); slots 64..71 are the
     // padding a batch of 8 may reach: -0 and +0, so a padded step
@@ -387,12 +458,14 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             uint32_t l = ~0u;
             int src = -1;
             bool ok = true;
-            if (t == 0) {
+            if (MR && wg != 0) {
+                // the rank's own decision is workgroup 0's; this workgroup only polls
+            } else if (t == 0) {
                 // candidates of the previous select (k_select_d, a bootstrap or the previous launch)
                 uint64_t mh = ~0ull, mp0 = 0, mp1 = 0;
                 uint32_t ml = ~0u;
-                for (int e = lane; e < a.ncand; e += 64) {
-                    const Cand cd = a.part[e];
+                for (int e = lane; e < a.ncin; e += 64) {
+                    const Cand cd = a.cin[e];
                     if (cd.row < 0) continue;
                     const uint64_t ch = (uint64_t)__double_as_longlong(cd.theta);
                     const uint32_t cl = (uint32_t)cd.key;
@@ -421,10 +494,21 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                     p1 = pay[0].z;              // leaving row
                 }
             }
+            int xfail = 0;
+            if (MR) {                           // every rank's best -> the grid's
+                const uint32_t xt = a.xtag0 + (uint32_t)t;
+                if (wg == 0 && ok && lane == 0)
+                    xpush_best(a.X, xt, src >= 0 ? h : ~0ull, src >= 0 ? l : ~0u, p0, p1);
+                if (ok && !xpoll_best(a.X, xt, h, l, p0, p1, st)) {
+                    ok = false;
+                    xfail = 1;
+                }
+                src = (h == ~0ull && l == ~0u) ? -1 : 0;
+            }
             if (lane == 0) {
                 bc.h = h;
                 bc.l = l;
-                bc.ok = !ok ? -1 : (src >= 0 ? 1 : 0);
+                bc.ok = !ok ? (xfail ? -2 : -1) : (src >= 0 ? 1 : 0);
                 bc.p0 = p0;
                 bc.p1 = p1;
             }
@@ -441,16 +525,20 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                 st->slot[s].status = sv;
                 st->slot[s].r = -1;
                 st->slot[s ^ 1].status = sv;
-                if (okP < 0) st->stall = 1;
+                if (okP < 0) st->stall = okP == -2 ? 2 : 1;
             }
             break;
         }
+        const bool own = !MR || (r >= g.row0 && r < g.row0 + g.nloc);   // uniform: this rank holds row r
+        const int64_t rl = MR ? (own ? r - g.row0 : -1) : r;           // its local index (-1: another rank's)
+        int64_t lvv = 0;                                // MR: the leaving variable, from the replicated basis
         // k_prep_d's bookkeeping, stores only (a dependent load here would hold
         // back workgroup 0, and every sweep waits for the slowest workgroup):
         // the row's owner records the leaving variable it holds
         if (wg == 0 && tid == 0) {
             st->slot[s].r = r;
-            D.rq[q] = r;
+            D.rq[q] = rl;
+            if (MR) lvv = D.basis[r];                   // stored after the chain: its latency hides there
             st->npend = q + 1;
             D.kq[q] = kt;
             D.pv[q] = piv;
@@ -463,23 +551,27 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             st->last_k = kt;
             st->last_r = r;
         }
-        if (hr && i == r) {
-            D.lv[q] = mybasis;
-            D.basis[r] = kt;
+        if (hr && i == rl) {
+            if (!MR) {
+                D.lv[q] = mybasis;
+                D.basis[r] = kt;
+            }
             mybasis = kt;
             lastpiv = q;
         }
         // multipliers -C_u[r] (lane u < q; -0 past q), the pivot row's restart point
-        wm[wave][lane] = lane < q ? -ld_wt(D.Cbuf + (int64_t)lane * D.cs + r) : -0.0;
-        const unsigned long long hit = __ballot(lane < q && rqv == r);
+        wm[wave][lane] = (own && lane < q) ? -ld_wt(D.Cbuf + (int64_t)lane * D.cs + rl) : -0.0;
+        const unsigned long long hit = __ballot(own && lane < q && rqv == rl);
         const int qs = hit ? 63 - __clzll((long long)hit) : -1;
-        if (lane == q) rqv = r;
-        double x = hc ? g.T[r * g.ld + c] : 0.0;
+        if (lane == q) rqv = rl;
+        double x = (own && hc) ? g.T[rl * g.ld + c] : 0.0;
         LPG_BPH(t, 2);
         // the pending chain over slots u < q (NS >= q), restarting after qs
         if (qs >= 0) x = sPt[qs];
         const double *wmw = &wm[wave][0];
-        if (qs < 0) {
+        if (!own) {
+            // another rank's row: its P slice arrives below
+        } else if (qs < 0) {
             if (q <= 16) x = chain_row<16, false>(sPt, wmw, qs, x);
             else if (q <= 32) x = chain_row<32, false>(sPt, wmw, qs, x);
             else if (q <= 48) x = chain_row<48, false>(sPt, wmw, qs, x);
@@ -493,8 +585,61 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         drain();                                        // the previous phase's C stores, before this record
         PricePart pb{0.0, -1, 0, 0};
         double pq = 0.0;
+        if (own && hc) pq = x / piv;
+        if (MR) {
+            const uint32_t xt = a.xtag0 + (uint32_t)t;
+            const int par = (int)(xt & 1);
+            if (own) {                                  // this slice of P to every other rank, then its flag
+                if (hc)
+                    for (int rk = 0; rk < a.X.world; rk++)
+                        if (rk != a.X.rank)
+                            st_sys64((double *)a.X.base[rk] + (int64_t)par * g.ld + c,
+                                     (uint64_t)__double_as_longlong(pq));
+                drain();
+                __syncthreads();
+                if (tid == 0) {
+                    __threadfence_system();
+                    for (int rk = 0; rk < a.X.world; rk++)
+                        if (rk != a.X.rank)
+                            __hip_atomic_store(xch_flag(a.X, rk, par, wg), xt, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            } else {                                    // wait for this slice of P from the owner
+                if (tid == 0) {
+                    const long long t0 = (long long)wall_clock64();
+                    int okx = 1;
+                    while (__hip_atomic_load(xch_flag(a.X, a.X.rank, par, wg), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM) != xt) {
+                        if ((long long)wall_clock64() - t0 > kSpinTicks) {
+                            okx = 0;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    __threadfence_system();
+                    xok = okx;
+                }
+                __syncthreads();
+                if (!xok) {
+                    if (tid == 0) {
+                        st->slot[s].status = NUMERIC;
+                        st->slot[s ^ 1].status = NUMERIC;
+                        st->stall_info[0] = 5;
+                        st->stall_info[1] = xt;
+                        st->stall = 3;
+                    }
+                    break;
+                }
+                if (hc)
+                    pq = __longlong_as_double(
+                        (long long)ld_sys64((const double *)a.X.base[a.X.rank] + (int64_t)par * g.ld + c));
+            }
+            if (wg == 0 && tid == 0) {                  // the replicated basis and the block's leaving variables
+                D.lv[q] = lvv;
+                D.basis[r] = kt;
+            }
+        }
         if (hc) {
-            pq = x / piv;
             sPt[q] = pq;
             st_wt(D.Pbuf + (int64_t)q * g.ld + c, pq);  // drained in phase S, before the ratio record
             if (NOBJ == 2) dM = fma(-cobjM, pq, dM);
@@ -588,7 +733,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         if (wave * 64 < rw)                             // waves holding rows
             wp[wave][lane] = lane < q ? ld_wt(D.Pbuf + (int64_t)lane * g.ld + kp) : (lane == q ? pkq : 0.0);
         LPG_BPH(t, 6);
-        if (hr) b = (i == r) ? p0q : fma(-sCt[q], p0q, b);
+        if (hr) b = (i == rl) ? p0q : fma(-sCt[q], p0q, b);
         // the chain over slots v <= q (NS > q). A row pivoted earlier in this
         // block restarts at its last pivot lp: x = P_lp[k] and the steps up to
         // lp become no-ops (the select form, for waves holding such a row).
@@ -688,9 +833,11 @@ int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, i
 }
 
 int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, int s0, int q0, int n, Cand *part,
-                       int ncand, const double *Cs0, double *Cs1, const Defer &D, void *rec, uint32_t tag0, int nwg,
-                       int cw, int rw, int ks, size_t lds) {
+                       int ncand, const Cand *cin, int ncin, const double *Cs0, double *Cs1, const Defer &D,
+                       void *rec, uint32_t tag0, int nwg, int cw, int rw, int ks, size_t lds, const Xch *X,
+                       uint32_t xtag0) {
     if (n < 1 || q0 < 0 || q0 + n > ks || ks > 64 || nwg < 1 || nwg > kMaxWG || ncand < nwg) return -1;
+    if (X && (X->world < 1 || X->world > 64 || X->nblk < nwg || X->nx < 1)) return -1;
     if ((int64_t)nwg * cw < ((g.ncols + 1) & ~(int64_t)1) || (int64_t)nwg * rw < g.nloc) return -1;
     if (g.nobj != 1 && g.nobj != 2) return -1;
     BlockArgs a;
@@ -702,6 +849,10 @@ int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, in
     a.n = n;
     a.part = part;
     a.ncand = ncand;
+    a.cin = cin;
+    a.ncin = ncin;
+    a.X = X ? *X : Xch{};
+    a.xtag0 = xtag0;
     a.Cs0 = Cs0;
     a.Cs1 = Cs1;
     a.D = D;
@@ -712,24 +863,30 @@ int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, in
     a.rw = rw;
     a.ks = ks;
     hipStream_t stream = (hipStream_t)L.stream;
-#define LPG_PB(R, NO)                                                                                   \
+#define LPG_PB(R, NO, M)                                                                                \
     do {                                                                                                \
         static bool attr = false;                                                                       \
         if (!attr) {                                                                                    \
-            if (hipFuncSetAttribute((const void *)k_pivot_block<R, NO>,                                 \
+            if (hipFuncSetAttribute((const void *)k_pivot_block<R, NO, M>,                              \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds) != hipSuccess) \
                 return -1;                                                                              \
             attr = true;                                                                                \
         }                                                                                               \
-        hipLaunchKernelGGL((k_pivot_block<R, NO>), dim3(nwg), dim3(kNT), lds, stream, a);              \
+        hipLaunchKernelGGL((k_pivot_block<R, NO, M>), dim3(nwg), dim3(kNT), lds, stream, a);           \
+    } while (0)
+#define LPG_PB_M(R, NO)              \
+    do {                             \
+        if (X) LPG_PB(R, NO, true);  \
+        else LPG_PB(R, NO, false);   \
     } while (0)
     if (rule == RULE_BLAND) {
-        if (g.nobj == 2) LPG_PB(RULE_BLAND, 2);
-        else LPG_PB(RULE_BLAND, 1);
+        if (g.nobj == 2) LPG_PB_M(RULE_BLAND, 2);
+        else LPG_PB_M(RULE_BLAND, 1);
     } else {
-        if (g.nobj == 2) LPG_PB(RULE_DANTZIG, 2);
-        else LPG_PB(RULE_DANTZIG, 1);
+        if (g.nobj == 2) LPG_PB_M(RULE_DANTZIG, 2);
+        else LPG_PB_M(RULE_DANTZIG, 1);
     }
+#undef LPG_PB_M
 #undef LPG_PB
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

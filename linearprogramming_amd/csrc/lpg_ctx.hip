@@ -63,7 +63,9 @@ struct lpg_ctx {
     int pivot_nt = kPivotThreads; // threads per block of that pair
     // the persistent block kernel (lpg_block.hip): single rank, deferred, the
     // default where its slices fit (LPG_PERSIST=0 turns it off)
-    bool persist = false;
+    bool persist = false;         // single rank, no communicator: k_pivot_block
+    bool pmr = false;             // k_pivot_block's geometry also holds for the multi-rank form (same on every rank)
+    bool persist_x = false;       // multi-rank k_pivot_block over the owner-push exchange (attach_push)
     int pb_nwg = 0, pb_cw = 0, pb_rw = 0;
     size_t pb_lds = 0;
     void *rec = nullptr;          // its records (zeroed once; tags never repeat within a context)
@@ -436,13 +438,38 @@ static int cand_cap(const lpg_ctx *c) { return std::max(c->nsel, c->nsel_d); }
 // block, the block's flush after its last pivot.
 static int enqueue_blocks(lpg_ctx *c, int64_t npiv, int rule) {
     const Geo g = geo(c);
+    const bool mr = c->persist_x && c->xmode;
     while (npiv > 0) {
         const int n = (int)std::min<int64_t>(npiv, c->defer_k - c->pend);
         const int s0 = c->par, s1 = (s0 + n) & 1;
-        if (launch_pivot_block(lau(c), g, rule, c->st, s0, c->pend, n, c->part, cand_cap(c), c->C[s0], c->C[s1],
+        // the first pivot's ratio candidates: the previous launch's (one per
+        // workgroup, this rank's) or, after a bootstrap on a communicator, the
+        // gathered ones of every rank
+        const Cand *cin = c->part;
+        int ncin = cand_cap(c), ncand = cand_cap(c);
+        Xch X;
+        if (mr) {
+            ncand = std::max(ncand, c->pb_nwg);
+            ncin = c->x_from_cand ? cand_per_rank(c) * c->world : c->pb_nwg;
+            if (c->x_from_cand) cin = c->cand;
+            X.base = c->xbase;
+            X.world = c->world;
+            X.rank = c->rank;
+            X.nblk = c->xnblk;
+            X.nx = c->xnx;
+            X.from_cand = 0;
+            X.tag = c->xtag;
+            X.offF = c->xoffF;
+            X.offC = c->xoffC;
+        }
+        if (launch_pivot_block(lau(c), g, rule, c->st, s0, c->pend, n, c->part, ncand, cin, ncin, c->C[s0], c->C[s1],
                                defer_of(c, c->pend), c->rec, c->tag, c->pb_nwg, c->pb_cw, c->pb_rw, c->defer_k,
-                               c->pb_lds))
+                               c->pb_lds, mr ? &X : nullptr, c->xtag))
             return fail(c, LPG_ERR_DEVICE, "pivot block launch failed");
+        if (mr) {
+            c->xtag += (uint32_t)n;
+            c->x_from_cand = false;
+        }
         c->tag += (uint32_t)n;
         c->pend += n;
         c->par = s1;
@@ -506,6 +533,7 @@ static int enqueue(lpg_ctx *c, int64_t npiv, int rule) {
         if (rc) return rc;
     }
     if (c->persist && !has_comm(c)) return enqueue_blocks(c, npiv, rule);
+    if (c->persist_x && c->xmode) return enqueue_blocks(c, npiv, rule);
     const int G = graph_len(c);
     // eager-mode timing brackets every update, which a graph cannot; deferred
     // timing brackets only the flushes, which stay outside the graph
@@ -780,13 +808,21 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     // same on every rank (the candidates are allgathered)
     c->nsel_d = world == 1 ? pivot_d_blocks(g, 1, c->pivot_nt) : (int)((maxloc + 255) / 256);
     {
+        // the split is computed for the largest row block, so every rank of a
+        // row partition gets the same workgroups, columns and rows per slice
+        // (the multi-rank form exchanges P slice by slice)
         const char *pe = getenv("LPG_PERSIST"), *pw = getenv("LPG_PERSIST_WG");
         int cus = 0;
-        if (world == 1 && c->defer_k > 0 && c->fast_pivot && !(pe && atoi(pe) == 0) &&
+        Geo gm = g;
+        gm.nloc = (m + world - 1) / world;
+        if (c->defer_k > 0 && c->fast_pivot && !(pe && atoi(pe) == 0) &&
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
-            block_geometry(g, c->defer_k, cus, pw ? atoi(pw) : 0, &c->pb_nwg, &c->pb_cw, &c->pb_rw, &c->pb_lds) == 0) {
-            c->persist = true;
-            c->nsel_d = c->pb_nwg;          // one ratio candidate per workgroup
+            block_geometry(gm, c->defer_k, cus, pw ? atoi(pw) : 0, &c->pb_nwg, &c->pb_cw, &c->pb_rw, &c->pb_lds) == 0) {
+            c->pmr = true;
+            if (world == 1) {
+                c->persist = true;
+                c->nsel_d = c->pb_nwg;      // one ratio candidate per workgroup
+            }
         }
     }
 #define ALLOC(p, bytes)                                                                    \
@@ -808,8 +844,8 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     ALLOC(c->cost, (size_t)ncols * sizeof(double));
     ALLOC(c->pp, (size_t)std::max(c->npp, c->npp_d) * sizeof(PricePart));
     ALLOC(c->pc, (size_t)c->npp * sizeof(int));
-    ALLOC(c->part, (size_t)std::max(c->nsel, c->nsel_d) * sizeof(Cand));
-    if (c->persist) ALLOC(c->rec, (size_t)block_records_bytes(c->pb_nwg));
+    ALLOC(c->part, (size_t)std::max({c->nsel, c->nsel_d, c->pmr ? c->pb_nwg : 0}) * sizeof(Cand));
+    if (c->pmr) ALLOC(c->rec, (size_t)block_records_bytes(c->pb_nwg));
     if (world > 1) ALLOC(c->cand, (size_t)std::max(c->nsel, c->nsel_d) * world * sizeof(Cand));
     else c->cand = c->part;
     ALLOC(c->basis, (size_t)m * sizeof(int64_t));
@@ -921,7 +957,7 @@ int lpg_comm_init_host(lpg_ctx *c, const lpg_host_comm_ops *ops) {
 static int ensure_xbuf(lpg_ctx *c) {
     if (c->xbuf) return 0;
     if (!(c->defer_k > 0 && c->fast_pivot)) return fail(c, LPG_ERR_STATE, "push exchange needs the deferred pivot pair");
-    c->xnblk = c->npp_d;
+    c->xnblk = std::max(c->npp_d, c->pmr ? c->pb_nwg : 0);   // P chunk flags: prep blocks / k_pivot_block slices
     c->xnx = c->nsel_d;
     c->xbytes = xch_bytes(c->ld, c->world, c->xnblk, c->xnx, &c->xoffF, &c->xoffC);
     // uncached: a peer's stores over xGMI land in this GPU's HBM behind its
@@ -944,6 +980,10 @@ static int attach_push(lpg_ctx *c, std::vector<char *> &bases) {
     graph_drop(c);
     c->xmode = true;
     c->booted = false;               // the next pivot bootstraps (its candidates through the communicator)
+    // the pivot loop as one launch per block on every rank (LPG_PERSIST=0 or
+    // LPG_PERSIST_MR=0: the two-kernel pair)
+    const char *pe = getenv("LPG_PERSIST"), *pm = getenv("LPG_PERSIST_MR");
+    c->persist_x = c->pmr && !(pe && atoi(pe) == 0) && !(pm && atoi(pm) == 0);
     return 0;
 }
 
@@ -1032,7 +1072,7 @@ int lpg_info(const lpg_ctx *c, lpg_info_t *o) {
     o->device = c->device;
     o->nobj = (int32_t)c->nobj;
     o->defer_k = c->defer_k;
-    o->pivot_wg = c->persist ? c->pb_nwg : 0;
+    o->pivot_wg = ((c->persist && !has_comm(c)) || (c->persist_x && c->xmode)) ? c->pb_nwg : 0;
     o->bytes_per_pivot = 16.0 * (double)(c->nloc + c->nobj) * (double)c->ncols;
     o->exchange = c->xmode ? (c->xuncached ? 2 : 1) : 0;
     o->pad2_ = 0;
@@ -1173,7 +1213,7 @@ int lpg_prepare(lpg_ctx *c, int rule) {
     if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
     if (!c->booted || c->boot_rule != rule)
         if ((rc = bootstrap(c, rule))) return rc;
-    if (c->persist && !has_comm(c)) return 0;   // one launch per block: nothing to capture
+    if ((c->persist && !has_comm(c)) || (c->persist_x && c->xmode)) return 0;   // one launch per block: nothing to capture
     // the conditions under which enqueue replays graphs (enqueue, above)
     const int G = graph_len(c);
     const bool timed = c->timing && c->defer_k == 0;

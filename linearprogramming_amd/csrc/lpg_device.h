@@ -247,4 +247,18 @@ __device__ __forceinline__ void price_one(PricePart &best, double dM, double dR,
     if (pp_better<RULE>(c, best)) best = c;
 }
 
+// ---- owner-push exchange (Xch, lpg_internal.h) ----
+__device__ __forceinline__ void st_sys64(void *p, uint64_t v) {
+    __hip_atomic_store((unsigned long long *)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys64(const void *p) {
+    return (uint64_t)__hip_atomic_load((unsigned long long *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t *xch_flag(const Xch &X, int rank, int par, int b) {
+    return (uint32_t *)(X.base[rank] + X.offF) + (int64_t)par * X.nblk + b;
+}
+__device__ __forceinline__ uint64_t *xch_cand(const Xch &X, int rank, int par, int from, int e) {
+    return (uint64_t *)(X.base[rank] + X.offC) + (((int64_t)par * X.world + from) * X.nx + e) * 6;
+}
+
 }  // namespace lpg

@@ -176,9 +176,13 @@ int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int 
 // block_records_bytes(nwg) zero-initialised bytes; tags start after tag0.
 int block_records_bytes(int nwg);
 int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, int *rw, size_t *lds);
+// cin / ncin: the first pivot's ratio candidates (part itself on one rank).
+// X != nullptr: multi-rank over the owner-push exchange (the same nwg / cw / rw
+// on every rank), exchange tags xtag0, xtag0 + 1, ...
 int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, int s0, int q0, int n, Cand *part,
-                       int ncand, const double *Cs0, double *Cs1, const Defer &D, void *rec, uint32_t tag0, int nwg,
-                       int cw, int rw, int ks, size_t lds);
+                       int ncand, const Cand *cin, int ncin, const double *Cs0, double *Cs1, const Defer &D,
+                       void *rec, uint32_t tag0, int nwg, int cw, int rw, int ks, size_t lds, const Xch *X = nullptr,
+                       uint32_t xtag0 = 0);
 // Apply the pending pivots (st->npend <= kmax) to constraint rows 0..nloc-1.
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which);
 // ... in two parts: the block pass itself (k_flushw / k_flushm / k_flush), then

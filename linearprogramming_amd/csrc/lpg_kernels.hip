@@ -602,19 +602,6 @@ __device__ unsigned long long g_ph[2][16];
 #define LPG_PH(kern, k) do { } while (0)
 #endif
 
-// ---- owner-push exchange (Xch, lpg_internal.h) ----
-__device__ __forceinline__ void st_sys64(void *p, uint64_t v) {
-    __hip_atomic_store((unsigned long long *)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint64_t ld_sys64(const void *p) {
-    return (uint64_t)__hip_atomic_load((unsigned long long *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint32_t *xch_flag(const Xch &X, int rank, int par, int b) {
-    return (uint32_t *)(X.base[rank] + X.offF) + (int64_t)par * X.nblk + b;
-}
-__device__ __forceinline__ uint64_t *xch_cand(const Xch &X, int rank, int par, int from, int e) {
-    return (uint64_t *)(X.base[rank] + X.offC) + (((int64_t)par * X.world + from) * X.nx + e) * 6;
-}
 constexpr long long kXSpinTicks = 200000000ll;     // s_memrealtime (100 MHz): 2 s, then NUMERIC + stall
 
 // The candidates of every rank for this pivot (tag X.tag), polled by the
@@ -1198,7 +1185,7 @@ int64_t xch_bytes(int64_t ld, int world, int nblk, int nx, int64_t *offF, int64_
 
 int launch_prep_x(const Launch &L, const Geo &g, int rule, DevState *st, int s, const Cand *cand, int ncand,
                   double *P, const double *Cs, PricePart *pp, int npp_d, const Defer &D, const Xch &X) {
-    if (npp_d != pivot_d_blocks(g, 0, 256) || X.nblk != npp_d) return -1;
+    if (npp_d != pivot_d_blocks(g, 0, 256) || X.nblk < npp_d) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
 #define LPG_PX(R, PF)                                                                                                 \
     hipLaunchKernelGGL((k_prep_d<R, PF, 256, 2>), dim3(npp_d), dim3(256), 0, stream, g.T, g, st, s, cand, ncand, P,    \

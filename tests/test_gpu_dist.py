@@ -112,9 +112,11 @@ def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule, defer, monk
     assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
 
 
-def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule=0, defer=None):
+def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule=0, defer=None, mr=None):
     if defer is not None:
         os.environ["LPG_DEFER"] = defer
+    if mr is not None:                            # 0: the two-kernel pair instead of k_pivot_block's multi-rank form
+        os.environ["LPG_PERSIST_MR"] = mr
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -142,20 +144,20 @@ def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule
     res = e.solve(5000, rule)
     info = e.info
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
-        pickle.dump(dict(status=res.status, pivots=res.pivots, log=e.get_log(), basis=e.get_basis(),
+        pickle.dump(dict(status=res.status, pivots=res.pivots, log=e.get_log(), basis=e.get_basis(), wg=info.pivot_wg,
                          rows=e.get_rows(info.row0, info.nrows), obj=e.get_rows(m, 1)[0]), f)
     e.close()
     dist.destroy_process_group()
 
 
-def _processes(world, m, n, seed, push, kind=0, rule=0, defer=None):
+def _processes(world, m, n, seed, push, kind=0, rule=0, defer=None, mr=None):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_gloo_worker, args=(world, port, m, n, seed, d, push, kind, rule, defer), nprocs=world, join=True)
+        mp.spawn(_gloo_worker, args=(world, port, m, n, seed, d, push, kind, rule, defer, mr), nprocs=world, join=True)
         parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     o = Oracle(m, n + m + 1)
     o.generate(n, seed, kind)
@@ -167,24 +169,34 @@ def _processes(world, m, n, seed, push, kind=0, rule=0, defer=None):
         assert np.array_equal(p["basis"], o.get_basis())
         assert np.array_equal(p["obj"], T[m])
     assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
+    return parts
 
 
 def test_two_processes_gloo_bitwise(lpg):
     _processes(2, 120, 200, 31, push=False)
 
 
+@pytest.mark.parametrize("mr", [None, "0"])
 @pytest.mark.parametrize("world,m,n,kind,rule,defer", [(2, 120, 200, 0, 0, None), (2, 96, 160, 0, 0, "5"),
                                                        (3, 101, 77, 0, 0, "64"), (2, 64, 64, 1, 1, "5"),
-                                                       (3, 203, 301, 0, 0, "32"), (2, 203, 301, 0, 0, "128")])
-def test_processes_owner_push_bitwise(lpg, world, m, n, kind, rule, defer):
+                                                       (3, 203, 301, 0, 0, "32"), (2, 203, 301, 0, 0, "128"),
+                                                       (2, 1024, 2048, 0, 0, None), (3, 700, 900, 1, 1, "64")])
+def test_processes_owner_push_bitwise(lpg, world, m, n, kind, rule, defer, mr):
     """The owner-push exchange between ranks in separate processes sharing the
     GPU (IPC-mapped exchange buffers, the layout of one process per GPU): no
     collective per pivot -- the owner stores the pivot row into every rank's
     buffer, every rank its candidates -- bitwise the oracle. (Ranks as threads
     of one process are not used here: a process gets GPU_MAX_HW_QUEUES = 4
     hardware queues, and two ranks' streams on one queue would serialise a
-    waiting kernel in front of the kernel it waits for.)"""
-    _processes(world, m, n, 778, push=True, kind=kind, rule=rule, defer=defer)
+    waiting kernel in front of the kernel it waits for.)
+    By default (mr None) every rank runs k_pivot_block's multi-rank form --
+    one launch per block, the leaving row and the pivot row exchanged inside
+    it -- wherever its slices fit (blocks of <= 64 pivots); mr "0" keeps the
+    two-kernel pair."""
+    parts = _processes(world, m, n, 778, push=True, kind=kind, rule=rule, defer=defer, mr=mr)
+    persistent = mr is None and (defer is None or int(defer) <= 64)
+    assert all((p["wg"] > 0) == persistent for p in parts)
+    assert len({p["wg"] for p in parts}) == 1          # the same slices on every rank
 
 
 @pytest.mark.parametrize("m,n,defer,graphs", [(300, 500, None, "0"), (1024, 2048, None, "0"), (1024, 2048, "64", "0"),
@@ -221,15 +233,19 @@ def test_host_comm_single_rank(lpg):
         e.comm_init_host(lambda b: b, lambda a: a)     # one communicator per context
 
 
+@pytest.mark.parametrize("mr", ["1", "0"])
 @pytest.mark.parametrize("m,n", [(300, 500), (1024, 2048)])
-def test_owner_push_single_rank(lpg, m, n, monkeypatch):
-    """The owner-push kernels on a 1-rank communicator (pushes to itself):
+def test_owner_push_single_rank(lpg, m, n, mr, monkeypatch):
+    """The owner-push exchange on a 1-rank communicator (pushes to itself):
+    k_pivot_block's multi-rank form (mr 1) and the two-kernel pair (mr 0),
     bitwise the engine without a communicator and the oracle."""
     monkeypatch.setenv("LPG_DEFER", "64")
+    monkeypatch.setenv("LPG_PERSIST_MR", mr)
     e = lpg.Engine(m, n + m + 1)
     e.comm_init_host(lambda b: b, lambda a: a)
     e.comm_init_push([e.push_handle()])
     assert e.info.exchange in (1, 2)                # 2: the exchange buffer is uncached (hipDeviceMallocUncached)
+    assert (e.info.pivot_wg > 0) == (mr == "1")
     print(f"exchange mode {e.info.exchange}")
     e.generate(n, 43, 0)
     res = e.solve(100_000, 0)
