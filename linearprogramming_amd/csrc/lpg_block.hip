@@ -453,14 +453,16 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         const uint32_t tag = a.tag0 + 1 + (uint32_t)t;
         LPG_BPH(t, 0);
         // ================= phase P: the leaving row and the pivot row
+        // MR: this rank's best ratio candidate goes to every rank, and while
+        // the grid's best is awaited every workgroup computes the pivot row
+        // of this rank's best row -- which is the grid's whenever this rank
+        // holds the grid's (the global minimum is one of the ranks' minima)
         if (wave == 0) {
             uint64_t h = ~0ull, p0 = 0, p1 = 0;
             uint32_t l = ~0u;
             int src = -1;
             bool ok = true;
-            if (MR && wg != 0) {
-                // the rank's own decision is workgroup 0's; this workgroup only polls
-            } else if (t == 0) {
+            if (t == 0) {
                 // candidates of the previous select (k_select_d, a bootstrap or the previous launch)
                 uint64_t mh = ~0ull, mp0 = 0, mp1 = 0;
                 uint32_t ml = ~0u;
@@ -494,43 +496,98 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                     p1 = pay[0].z;              // leaving row
                 }
             }
-            int xfail = 0;
-            if (MR) {                           // every rank's best -> the grid's
-                const uint32_t xt = a.xtag0 + (uint32_t)t;
-                if (wg == 0 && ok && lane == 0)
-                    xpush_best(a.X, xt, src >= 0 ? h : ~0ull, src >= 0 ? l : ~0u, p0, p1);
-                if (ok && !xpoll_best(a.X, xt, h, l, p0, p1, st)) {
-                    ok = false;
-                    xfail = 1;
-                }
-                src = (h == ~0ull && l == ~0u) ? -1 : 0;
-            }
+            if (MR && wg == 0 && ok && lane == 0)   // this rank's best -> every rank
+                xpush_best(a.X, a.xtag0 + (uint32_t)t, src >= 0 ? h : ~0ull, src >= 0 ? l : ~0u, p0, p1);
             if (lane == 0) {
                 bc.h = h;
                 bc.l = l;
-                bc.ok = !ok ? (xfail ? -2 : -1) : (src >= 0 ? 1 : 0);
+                bc.ok = !ok ? -1 : (src >= 0 ? 1 : 0);
                 bc.p0 = p0;
                 bc.p1 = p1;
             }
         }
         __syncthreads();
         LPG_BPH(t, 1);
-        const int okP = bc.ok;
-        const double piv = __longlong_as_double((long long)bc.p0);
-        const int64_t r = (int64_t)bc.p1;               // leaving row (local == global: one rank)
-        __syncthreads();                                // bc is rewritten by the next phase
-        if (okP <= 0 || !isfinite(piv)) {               // the oracle's NUMERIC rule (k_prep_d)
+        int okP = bc.ok;
+        double piv = __longlong_as_double((long long)bc.p0);
+        int64_t r = (int64_t)bc.p1;                     // leaving row (MR: this rank's candidate so far)
+        __syncthreads();                                // bc is rewritten below / by the next phase
+        auto fail_p = [&](int ok) {                     // the oracle's NUMERIC rule (k_prep_d), UNBOUNDED, timeouts
             if (wg == 0 && tid == 0) {
-                const int32_t sv = okP < 0 ? NUMERIC : (okP == 0 ? UNBOUNDED : NUMERIC);
+                const int32_t sv = ok < 0 ? NUMERIC : (ok == 0 ? UNBOUNDED : NUMERIC);
                 st->slot[s].status = sv;
                 st->slot[s].r = -1;
                 st->slot[s ^ 1].status = sv;
-                if (okP < 0) st->stall = okP == -2 ? 2 : 1;
+                if (ok < 0) st->stall = ok == -2 ? 2 : 1;
             }
+        };
+        if (!MR && (okP <= 0 || !isfinite(piv))) {
+            fail_p(okP);
             break;
+        }
+        // row rr of the current tableau on this slice (on: this rank holds it):
+        // the multipliers -C_u[rr] (lane u < q; -0 past q), the restart point
+        // (the last pending pivot on rr), the base entries, the pending chain
+        auto pivot_row = [&](bool on, int64_t rr) -> double {
+            wm[wave][lane] = (on && lane < q) ? -ld_wt(D.Cbuf + (int64_t)lane * D.cs + rr) : -0.0;
+            const unsigned long long hit = __ballot(on && lane < q && rqv == rr);
+            const int qs = hit ? 63 - __clzll((long long)hit) : -1;
+            double x = (on && hc) ? g.T[rr * g.ld + c] : 0.0;
+            if (qs >= 0) x = sPt[qs];
+            const double *wmw = &wm[wave][0];
+            if (!on) {
+                // another rank's row: its P slice arrives below
+            } else if (qs < 0) {
+                if (q <= 16) x = chain_row<16, false>(sPt, wmw, qs, x);
+                else if (q <= 32) x = chain_row<32, false>(sPt, wmw, qs, x);
+                else if (q <= 48) x = chain_row<48, false>(sPt, wmw, qs, x);
+                else x = chain_row<64, false>(sPt, wmw, qs, x);
+            } else {
+                if (q <= 16) x = chain_row<16, true>(sPt, wmw, qs, x);
+                else if (q <= 32) x = chain_row<32, true>(sPt, wmw, qs, x);
+                else if (q <= 48) x = chain_row<48, true>(sPt, wmw, qs, x);
+                else x = chain_row<64, true>(sPt, wmw, qs, x);
+            }
+            return x;
+        };
+        const int64_t rs = r;                           // MR: the row computed ahead of the decision
+        const bool owns = okP > 0 && (!MR || (rs >= g.row0 && rs < g.row0 + g.nloc));
+        double x = pivot_row(owns, owns ? rs - g.row0 : -1);
+        LPG_BPH(t, 2);
+        if (MR) {                                       // every rank's best -> the grid's
+            if (wave == 0) {
+                uint64_t h = ~0ull, p0 = 0, p1 = 0;
+                uint32_t l = ~0u;
+                const bool ok = okP >= 0 && xpoll_best(a.X, a.xtag0 + (uint32_t)t, h, l, p0, p1, st);
+                if (lane == 0) {
+                    bc.ok = okP < 0 ? -1 : (!ok ? -2 : ((h == ~0ull && l == ~0u) ? 0 : 1));
+                    bc.p0 = p0;
+                    bc.p1 = p1;
+                }
+            }
+            __syncthreads();
+            okP = bc.ok;
+            piv = __longlong_as_double((long long)bc.p0);
+            r = (int64_t)bc.p1;
+            __syncthreads();
+            if (okP <= 0 || !isfinite(piv)) {
+                fail_p(okP);
+                break;
+            }
         }
         const bool own = !MR || (r >= g.row0 && r < g.row0 + g.nloc);   // uniform: this rank holds row r
         const int64_t rl = MR ? (own ? r - g.row0 : -1) : r;           // its local index (-1: another rank's)
+        if (MR && own && !(owns && r == rs)) {
+            // cannot happen: the grid's minimum, if this rank holds it, is this
+            // rank's minimum (unique keys). Stop loudly rather than guess.
+            if (tid == 0) {
+                st->slot[s].status = NUMERIC;
+                st->slot[s ^ 1].status = NUMERIC;
+                st->stall_info[0] = 6;
+                st->stall = 1;
+            }
+            break;
+        }
         int64_t lvv = 0;                                // MR: the leaving variable, from the replicated basis
         // k_prep_d's bookkeeping, stores only (a dependent load here would hold
         // back workgroup 0, and every sweep waits for the slowest workgroup):
@@ -538,7 +595,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         if (wg == 0 && tid == 0) {
             st->slot[s].r = r;
             D.rq[q] = rl;
-            if (MR) lvv = D.basis[r];                   // stored after the chain: its latency hides there
+            if (MR) lvv = D.basis[r];                   // stored after the P exchange: its latency hides there
             st->npend = q + 1;
             D.kq[q] = kt;
             D.pv[q] = piv;
@@ -559,29 +616,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             mybasis = kt;
             lastpiv = q;
         }
-        // multipliers -C_u[r] (lane u < q; -0 past q), the pivot row's restart point
-        wm[wave][lane] = (own && lane < q) ? -ld_wt(D.Cbuf + (int64_t)lane * D.cs + rl) : -0.0;
-        const unsigned long long hit = __ballot(own && lane < q && rqv == rl);
-        const int qs = hit ? 63 - __clzll((long long)hit) : -1;
         if (lane == q) rqv = rl;
-        double x = (own && hc) ? g.T[rl * g.ld + c] : 0.0;
-        LPG_BPH(t, 2);
-        // the pending chain over slots u < q (NS >= q), restarting after qs
-        if (qs >= 0) x = sPt[qs];
-        const double *wmw = &wm[wave][0];
-        if (!own) {
-            // another rank's row: its P slice arrives below
-        } else if (qs < 0) {
-            if (q <= 16) x = chain_row<16, false>(sPt, wmw, qs, x);
-            else if (q <= 32) x = chain_row<32, false>(sPt, wmw, qs, x);
-            else if (q <= 48) x = chain_row<48, false>(sPt, wmw, qs, x);
-            else x = chain_row<64, false>(sPt, wmw, qs, x);
-        } else {
-            if (q <= 16) x = chain_row<16, true>(sPt, wmw, qs, x);
-            else if (q <= 32) x = chain_row<32, true>(sPt, wmw, qs, x);
-            else if (q <= 48) x = chain_row<48, true>(sPt, wmw, qs, x);
-            else x = chain_row<64, true>(sPt, wmw, qs, x);
-        }
         drain();                                        // the previous phase's C stores, before this record
         PricePart pb{0.0, -1, 0, 0};
         double pq = 0.0;
@@ -589,7 +624,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         if (MR) {
             const uint32_t xt = a.xtag0 + (uint32_t)t;
             const int par = (int)(xt & 1);
-            if (own) {                                  // this slice of P to every other rank, then its flag
+            if (own && a.X.world > 1) {                 // this slice of P to every other rank, then its flag
                 if (hc)
                     for (int rk = 0; rk < a.X.world; rk++)
                         if (rk != a.X.rank)
@@ -598,13 +633,13 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                 drain();
                 __syncthreads();
                 if (tid == 0) {
-                    __threadfence_system();
+                    release_system();
                     for (int rk = 0; rk < a.X.world; rk++)
                         if (rk != a.X.rank)
                             __hip_atomic_store(xch_flag(a.X, rk, par, wg), xt, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_SYSTEM);
                 }
-            } else {                                    // wait for this slice of P from the owner
+            } else if (!own) {                          // wait for this slice of P from the owner
                 if (tid == 0) {
                     const long long t0 = (long long)wall_clock64();
                     int okx = 1;
@@ -616,8 +651,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                         }
                         __builtin_amdgcn_s_sleep(1);
                     }
-                    __threadfence_system();
-                    xok = okx;
+                    xok = okx;                          // the slice is read with system-scope loads: no acquire
                 }
                 __syncthreads();
                 if (!xok) {

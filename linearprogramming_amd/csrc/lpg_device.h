@@ -261,4 +261,18 @@ __device__ __forceinline__ uint64_t *xch_cand(const Xch &X, int rank, int par, i
     return (uint64_t *)(X.base[rank] + X.offC) + (((int64_t)par * X.world + from) * X.nx + e) * 6;
 }
 
+// Producer side of a cross-rank hand-off: the payload went out as
+// system-scope (sc0 sc1) stores and every storing wave waited for them
+// (s_waitcnt vmcnt(0), then a workgroup barrier); a system-scope RELEASE
+// (buffer_wbl2 sc0 sc1, ~1.7 us) then the flag. The wait after the fence is
+// inline asm so that the compiler cannot drop it (MI355X_MICROARCH.md,
+// "Compiler hazard"). The consumer needs no acquire: it polls the flag and
+// reads the payload with system-scope loads only, from uncached memory (the
+// guide's "sc1 loads replace the acquire" form); __threadfence_system() is
+// acq_rel (write-back AND invalidate, ~3.5 us) and was paid on both sides.
+__device__ __forceinline__ void release_system() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 }  // namespace lpg

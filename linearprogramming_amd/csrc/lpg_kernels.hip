@@ -816,7 +816,7 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (threadIdx.x == 0) {
-                __threadfence_system();
+                release_system();
                 for (int rk = 0; rk < X.world; rk++)
                     if (rk != X.rank)
                         __hip_atomic_store(xch_flag(X, rk, par, blockIdx.x), X.tag, __ATOMIC_RELAXED,
@@ -835,8 +835,7 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
-                __threadfence_system();
-                xok = ok;
+                xok = ok;                  // the chunk is read with system-scope loads: no acquire
             }
             __syncthreads();
             if (!xok) {
