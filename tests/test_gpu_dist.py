@@ -21,7 +21,7 @@ import threading
 import numpy as np
 import pytest
 
-from oracle.lpo import Oracle
+from oracle.lpo import GEN_ARTIFICIAL, Oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -112,7 +112,7 @@ def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule, defer, monk
     assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
 
 
-def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule=0, defer=None, mr=None):
+def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule=0, defer=None, mr=None, big_m=False):
     if defer is not None:
         os.environ["LPG_DEFER"] = defer
     if mr is not None:                            # 0: the two-kernel pair instead of k_pivot_block's multi-rank form
@@ -135,45 +135,65 @@ def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t.numpy()
 
-    e = lpg.Engine(m, n + m + 1, world=world, rank=rank)
+    e = lpg.Engine(m, n + m + 1, world=world, rank=rank, flags=lpg._lib.FLAG_BIG_M if big_m else 0)
     e.comm_init_host(allgather, allreduce)
     if push:                                      # owner-push exchange through IPC handles
         h = allgather(e.push_handle())
         e.comm_init_push([h[64 * r:64 * r + 64] for r in range(world)])
-    e.generate(n, seed, kind)
-    res = e.solve(5000, rule)
+    if big_m:                                     # two objective rows (M part, real part)
+        e.generate(n, seed, lpg.GEN_ARTIFICIAL)
+        res = e.solve_big_m(1 + n + (m + 1) // 2, None, 5000, rule)
+    else:
+        e.generate(n, seed, kind)
+        res = e.solve(5000, rule)
     info = e.info
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump(dict(status=res.status, pivots=res.pivots, log=e.get_log(), basis=e.get_basis(), wg=info.pivot_wg,
-                         rows=e.get_rows(info.row0, info.nrows), obj=e.get_rows(m, 1)[0]), f)
+                         rows=e.get_rows(info.row0, info.nrows), obj=e.get_rows(m, 2 if big_m else 1)), f)
     e.close()
     dist.destroy_process_group()
 
 
-def _processes(world, m, n, seed, push, kind=0, rule=0, defer=None, mr=None):
+def _processes(world, m, n, seed, push, kind=0, rule=0, defer=None, mr=None, big_m=False):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_gloo_worker, args=(world, port, m, n, seed, d, push, kind, rule, defer, mr), nprocs=world, join=True)
+        mp.spawn(_gloo_worker, args=(world, port, m, n, seed, d, push, kind, rule, defer, mr, big_m), nprocs=world,
+                 join=True)
         parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
-    o = Oracle(m, n + m + 1)
-    o.generate(n, seed, kind)
-    ores = o.solve(5000, rule)
+    if big_m:
+        o = Oracle(m, n + m + 1, nobj=2)
+        o.generate(n, seed, GEN_ARTIFICIAL)
+        ores = o.solve_big_m(1 + n + (m + 1) // 2, None, 5000, rule)
+    else:
+        o = Oracle(m, n + m + 1)
+        o.generate(n, seed, kind)
+        ores = o.solve(5000, rule)
     T = o.get_rows()
     for p in parts:
         assert p["status"] == ores.status and p["pivots"] == ores.pivots
         assert np.array_equal(p["log"][0], o.get_log()[0]) and np.array_equal(p["log"][1], o.get_log()[1])
         assert np.array_equal(p["basis"], o.get_basis())
-        assert np.array_equal(p["obj"], T[m])
+        assert np.array_equal(p["obj"], T[m:m + (2 if big_m else 1)])
     assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
     return parts
 
 
 def test_two_processes_gloo_bitwise(lpg):
     _processes(2, 120, 200, 31, push=False)
+
+
+@pytest.mark.parametrize("push,mr", [(False, None), (True, None), (True, "0")])
+@pytest.mark.parametrize("world,m,n,rule", [(2, 257, 300, 0), (3, 640, 512, 1)])
+def test_processes_big_m_bitwise(lpg, world, m, n, rule, push, mr):
+    """Big-M (two objective rows, lexicographic pricing) over 2-3 processes:
+    the collectives, the owner push with the multi-rank pivot launch (its
+    NOBJ = 2 form) and with the pair -- bitwise the oracle."""
+    parts = _processes(world, m, n, 9, push=push, rule=rule, mr=mr, big_m=True)
+    assert all((p["wg"] > 0) == (push and mr is None) for p in parts)
 
 
 @pytest.mark.parametrize("mr", [None, "0"])
