@@ -29,7 +29,7 @@ e.enqueue(K, 0)                      # one launch of K pivots
 torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * (2 * 64 * 8 + 2 * 64 * 256))()
 assert lib.lpg_debug_block_phases(buf) == 0
-names = ["P-sweep", "row-load", "P-chain+publish", "S-sweep", "S-load", "S-chain", "S-publish", "->next"]
+names = ["P-sweep", "row-load+chain", "P-publish", "S-sweep", "S-load", "S-chain", "S-publish", "->next"]
 for w in (0, 1):
     st = [[buf[(w * 64 + t) * 8 + k] for k in range(8)] for t in range(K)]
     print(f"workgroup {'0' if w == 0 else 'nwg/2'}: us per phase (10 ns ticks), by pivot range")
