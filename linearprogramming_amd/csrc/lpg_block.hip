@@ -70,6 +70,9 @@ constexpr int kRecPMax = 5;         // pricing record granules (k_pivot_block's 
 constexpr int kRecR = 2;            // ratio record:   {theta, key, tag} {piv, row, tag}
 constexpr int kMaxLds = 150 * 1024;   // dynamic LDS cap (the slices)
 constexpr long long kSpinTicks = 200000000ll;   // s_memrealtime runs at 100 MHz: 2 s
+#ifndef LPG_SWEEP_SLEEP
+#define LPG_SWEEP_SLEEP 1           // s_sleep between record polls (64 clocks each)
+#endif
 
 // doubles per thread row of the LDS slices: the unrolled chains read 16, 32,
 // 48 or 64 slots, so >= ks rounded up to 16; = 2 mod 4 (16-byte reads at this
@@ -150,7 +153,7 @@ __device__ bool sweep(__amdgpu_buffer_rsrc_t r, int nwg, uint32_t tag, u4 (&rec)
             }
             return false;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(LPG_SWEEP_SLEEP);
     }
 }
 
