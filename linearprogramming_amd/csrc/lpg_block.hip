@@ -557,6 +557,29 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         const bool owns = okP > 0 && (!MR || (rs >= g.row0 && rs < g.row0 + g.nloc));
         double x = pivot_row(owns, owns ? rs - g.row0 : -1);
         LPG_BPH(t, 2);
+        const uint32_t xt = a.xtag0 + (uint32_t)t;      // MR: this pivot's exchange tag
+        const int xpar = (int)(xt & 1);
+        if (MR && owns && a.X.world > 1) {
+            // every rank with a candidate sends ITS pivot row slice to every
+            // other rank (into the sender's own region, behind a per-slice
+            // flag) before the decision is known: the owner's copy, the one
+            // the others will read, is then already on its way while the
+            // decision travels (the other copies are never read)
+            if (hc) {
+                const uint64_t v = (uint64_t)__double_as_longlong(x / piv);
+                for (int rk = 0; rk < a.X.world; rk++)
+                    if (rk != a.X.rank) st_sys64(xch_row(a.X, rk, xpar, a.X.rank, g.ld) + c, v);
+            }
+            drain();
+            __syncthreads();
+            if (tid == 0) {
+                release_system();
+                for (int rk = 0; rk < a.X.world; rk++)
+                    if (rk != a.X.rank)
+                        __hip_atomic_store(xch_flag(a.X, rk, xpar, wg, a.X.rank), xt, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
         if (MR) {                                       // every rank's best -> the grid's
             if (wave == 0) {
                 uint64_t h = ~0ull, p0 = 0, p1 = 0;
@@ -625,28 +648,14 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         double pq = 0.0;
         if (own && hc) pq = x / piv;
         if (MR) {
-            const uint32_t xt = a.xtag0 + (uint32_t)t;
-            const int par = (int)(xt & 1);
-            if (own && a.X.world > 1) {                 // this slice of P to every other rank, then its flag
-                if (hc)
-                    for (int rk = 0; rk < a.X.world; rk++)
-                        if (rk != a.X.rank)
-                            st_sys64((double *)a.X.base[rk] + (int64_t)par * g.ld + c,
-                                     (uint64_t)__double_as_longlong(pq));
-                drain();
-                __syncthreads();
-                if (tid == 0) {
-                    release_system();
-                    for (int rk = 0; rk < a.X.world; rk++)
-                        if (rk != a.X.rank)
-                            __hip_atomic_store(xch_flag(a.X, rk, par, wg), xt, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-            } else if (!own) {                          // wait for this slice of P from the owner
+            if (!own) {                                 // wait for this slice of P from the owner
+                // the owner: rows [floor(m p / W), floor(m (p + 1) / W)) are rank p's
+                int owner = (int)((r * (int64_t)a.X.world) / g.m);
+                while (owner + 1 < a.X.world && (g.m * (int64_t)(owner + 1)) / a.X.world <= r) owner++;
                 if (tid == 0) {
                     const long long t0 = (long long)wall_clock64();
                     int okx = 1;
-                    while (__hip_atomic_load(xch_flag(a.X, a.X.rank, par, wg), __ATOMIC_RELAXED,
+                    while (__hip_atomic_load(xch_flag(a.X, a.X.rank, xpar, wg, owner), __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_SYSTEM) != xt) {
                         if ((long long)wall_clock64() - t0 > kSpinTicks) {
                             okx = 0;
@@ -667,9 +676,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                     }
                     break;
                 }
-                if (hc)
-                    pq = __longlong_as_double(
-                        (long long)ld_sys64((const double *)a.X.base[a.X.rank] + (int64_t)par * g.ld + c));
+                if (hc) pq = __longlong_as_double((long long)ld_sys64(xch_row(a.X, a.X.rank, xpar, owner, g.ld) + c));
             }
             if (wg == 0 && tid == 0) {                  // the replicated basis and the block's leaving variables
                 D.lv[q] = lvv;

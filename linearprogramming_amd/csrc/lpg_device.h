@@ -254,8 +254,13 @@ __device__ __forceinline__ void st_sys64(void *p, uint64_t v) {
 __device__ __forceinline__ uint64_t ld_sys64(const void *p) {
     return (uint64_t)__hip_atomic_load((unsigned long long *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ uint32_t *xch_flag(const Xch &X, int rank, int par, int b) {
-    return (uint32_t *)(X.base[rank] + X.offF) + (int64_t)par * X.nblk + b;
+// xP[par][src][ld]: the pivot row as stored by rank src (the pair uses src 0);
+// xF[par][src][nblk]: its chunk flags
+__device__ __forceinline__ double *xch_row(const Xch &X, int rank, int par, int src, int64_t ld) {
+    return (double *)X.base[rank] + ((int64_t)par * X.world + src) * ld;
+}
+__device__ __forceinline__ uint32_t *xch_flag(const Xch &X, int rank, int par, int b, int src = 0) {
+    return (uint32_t *)(X.base[rank] + X.offF) + ((int64_t)par * X.world + src) * X.nblk + b;
 }
 __device__ __forceinline__ uint64_t *xch_cand(const Xch &X, int rank, int par, int from, int e) {
     return (uint64_t *)(X.base[rank] + X.offC) + (((int64_t)par * X.world + from) * X.nx + e) * 6;

@@ -809,7 +809,7 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
             if (col)
                 for (int rk = 0; rk < X.world; rk++) {
                     if (rk == X.rank) continue;
-                    double *xp = (double *)X.base[rk] + (int64_t)par * g.ld + 2 * j2;
+                    double *xp = xch_row(X, rk, par, 0, g.ld) + 2 * j2;
                     st_sys64(xp, (uint64_t)__double_as_longlong(p.x));
                     st_sys64(xp + 1, (uint64_t)__double_as_longlong(p.y));
                 }
@@ -846,7 +846,7 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
                 return;
             }
             if (col) {
-                const double *xp = (const double *)X.base[X.rank] + (int64_t)par * g.ld + 2 * j2;
+                const double *xp = xch_row(X, X.rank, par, 0, g.ld) + 2 * j2;
                 p.x = __longlong_as_double((long long)ld_sys64(xp));
                 p.y = __longlong_as_double((long long)ld_sys64(xp + 1));
             }
@@ -1175,8 +1175,8 @@ int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int 
 
 // Owner-push exchange: the buffer's size and the offsets of its parts (256-byte aligned).
 int64_t xch_bytes(int64_t ld, int world, int nblk, int nx, int64_t *offF, int64_t *offC) {
-    const int64_t f = (2 * ld * (int64_t)sizeof(double) + 255) & ~(int64_t)255;
-    const int64_t c = (f + 2 * (int64_t)nblk * 4 + 255) & ~(int64_t)255;
+    const int64_t f = (2 * (int64_t)world * ld * (int64_t)sizeof(double) + 255) & ~(int64_t)255;   // xP[2][world][ld]
+    const int64_t c = (f + 2 * (int64_t)world * nblk * 4 + 255) & ~(int64_t)255;                  // xF[2][world][nblk]
     if (offF) *offF = f;
     if (offC) *offC = c;
     return c + 2 * (int64_t)world * nx * 6 * 8;
