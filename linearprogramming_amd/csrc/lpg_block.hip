@@ -1,5 +1,6 @@
 // lpg_block.hip — the deferred pivot loop as ONE persistent launch per run of
-// pivots (single rank, no communicator): k_pivot_block.
+// pivots: k_pivot_block (single rank; and, with MR, every rank of a row
+// partition over the owner-push exchange -- see the note above the kernel).
 //
 // What it replaces. Without it every pivot t is two kernels (k_prep_d, then
 // k_select_d, lpg_kernels.hip), and the kernel boundary between them is the
@@ -47,7 +48,8 @@
 // DevState::stall, and the launch drains.
 //
 // Residency: one workgroup per CU (the LDS slices force it), as many
-// workgroups as CUs; the launch needs the whole GPU to itself.
+// workgroups as CUs; the launch needs the whole GPU to itself (multi-rank:
+// each rank its own GPU, or launches small enough to be resident together).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
