@@ -270,10 +270,15 @@ __device__ bool xpoll_best(const Xch &X, uint32_t tag, uint64_t &h, uint32_t &l,
 // Phase probe (tools/block_probe.py; tools/liblpg_phases.so only): s_memrealtime
 // stamps of thread 0 of workgroups 0 and nwg / 2 at the phase boundaries of
 // every pivot of the launch.
-__device__ unsigned long long g_bph[2][64][8];
+__device__ unsigned long long g_bph[2][64][16];
+#ifdef LPG_PHASES_NOWAIT   // issue-time stamps: no wait for outstanding vector memory ops
+#define LPG_BPH_WAIT() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#else                      // completion stamps: everything issued so far has landed
+#define LPG_BPH_WAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
+#endif
 #define LPG_BPH(t, k)                                                                          \
     do {                                                                                       \
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                            \
+        LPG_BPH_WAIT();                                                                        \
         if (tid == 0 && (wg == 0 || wg == nwg / 2) && (t) < 64)                                \
             g_bph[wg == 0 ? 0 : 1][(t)][(k)] = __builtin_amdgcn_s_memrealtime();               \
     } while (0)
@@ -645,7 +650,9 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             lastpiv = q;
         }
         if (lane == q) rqv = rl;
+        LPG_BPH(t, 8);
         drain();                                        // the previous phase's C stores, before this record
+        LPG_BPH(t, 9);
         PricePart pb{0.0, -1, 0, 0};
         double pq = 0.0;
         if (own && hc) pq = x / piv;
@@ -693,7 +700,9 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             price_one<RULE>(pb, dM, dR, lj, g, c);
             pb.pad = (int32_t)c;
         }
+        LPG_BPH(t, 10);
         pb = block_argmin_pp<RULE, kNT / 64>(pb);
+        LPG_BPH(t, 11);
         if (tid == 0) {
             uint64_t h = ~0ull;
             uint32_t l = ~0u;
@@ -801,6 +810,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         }
         LPG_BPH(t, 7);
         drain();                                        // this pivot's P stores, before the ratio record
+        LPG_BPH(t, 12);
         const bool last = t + 1 == a.n;
         Cand cd{0.0, 0.0, 0, -1};
         if (hr) {
@@ -817,7 +827,9 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                 cd.key = RULE == RULE_BLAND ? mybasis : g.row0 + i;
             }
         }
+        LPG_BPH(t, 13);
         cd = block_argmin_cand<kNT / 64>(cd);
+        LPG_BPH(t, 14);
         if (tid == 0) {
             uint64_t h = ~0ull;
             uint32_t l = ~0u;

@@ -27,19 +27,25 @@ e.reserve_log(4 * K + 8)
 e.solve(2 * K, 0)                    # warm: bootstrap + two blocks, flushed
 e.enqueue(K, 0)                      # one launch of K pivots
 torch.cuda.synchronize()
-buf = (ctypes.c_ulonglong * (2 * 64 * 8 + 2 * 64 * 256))()
+NS = 16                              # stamp slots per pivot (lpg_block.hip g_bph)
+buf = (ctypes.c_ulonglong * (2 * 64 * NS + 2 * 64 * 256))()
 assert lib.lpg_debug_block_phases(buf) == 0
-names = ["P-sweep", "row-load+chain", "P-publish", "S-sweep", "S-load", "S-chain", "S-publish", "->next"]
+# stamp ids in time order within a pivot: 0 top, 1 ratio decision known, 2 pivot row (loads + chain),
+# 8 bookkeeping done, 9 drain, 10 P / d / pricing computed, 11 slice argmin, 3 pricing record published,
+# 4 pricing decision known, 6 column loads in, 7 column chain, 12 drain, 13 C / ratio candidate,
+# 14 slice argmin, 5 ratio record published; then the next pivot's 0
+order = [0, 1, 2, 8, 9, 10, 11, 3, 4, 6, 7, 12, 13, 14, 5]
+names = ["P-sweep", "row-load+chain", "bookkeeping", "P-drain", "P/d/price", "P-argmin", "P-store",
+         "S-sweep", "S-load", "S-chain", "S-drain", "C/cand", "S-argmin", "S-store", "->next"]
 for w in (0, 1):
-    st = [[buf[(w * 64 + t) * 8 + k] for k in range(8)] for t in range(K)]
+    st = [[buf[(w * 64 + t) * NS + k] for k in range(NS)] for t in range(K)]
     print(f"workgroup {'0' if w == 0 else 'nwg/2'}: us per phase (10 ns ticks), by pivot range")
     for lo, hi in ((0, 1), (1, 16), (16, 32), (32, 48), (48, K)):
-        acc = [0.0] * 8
+        acc = [0.0] * len(names)
         cnt = 0
         for t in range(lo, min(hi, K)):
             nxt = st[t + 1][0] if t + 1 < K else st[t][5]
-            d = [st[t][1] - st[t][0], st[t][2] - st[t][1], st[t][3] - st[t][2], st[t][4] - st[t][3],
-                 st[t][6] - st[t][4], st[t][7] - st[t][6], st[t][5] - st[t][7], nxt - st[t][5]]
+            d = [st[t][order[i + 1]] - st[t][order[i]] for i in range(len(order) - 1)] + [nxt - st[t][5]]
             acc = [a + x * 0.01 for a, x in zip(acc, d)]
             cnt += 1
         print(f"  t in [{lo:2d},{hi:2d}): " + " ".join(f"{nm}={a / cnt:.2f}" for nm, a in zip(names, acc)) +
@@ -48,7 +54,7 @@ for w in (0, 1):
 
 # publish skew: per pivot, every workgroup's record-store stamp (phase P and S)
 nwg = e.info.pivot_wg
-base = 2 * 64 * 8
+base = 2 * 64 * NS
 for ph, nm in ((0, "P"), (1, "S")):
     spread, late = [], {}
     for t in range(1, K):
