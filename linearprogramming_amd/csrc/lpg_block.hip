@@ -701,7 +701,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             pb.pad = (int32_t)c;
         }
         LPG_BPH(t, 10);
-        pb = block_argmin_pp<RULE, kNT / 64>(pb);
+        pb = block_argmin_pp<RULE, kNT / 64, false>(pb);   // barriers since the previous call: no lead
         LPG_BPH(t, 11);
         if (tid == 0) {
             uint64_t h = ~0ull;
@@ -828,7 +828,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             }
         }
         LPG_BPH(t, 13);
-        cd = block_argmin_cand<kNT / 64>(cd);
+        cd = block_argmin_cand<kNT / 64, false>(cd);
         LPG_BPH(t, 14);
         if (tid == 0) {
             uint64_t h = ~0ull;

@@ -97,29 +97,18 @@ __device__ PricePart block_reduce_pp(PricePart p) {
 // (v < 0, so ~bits orders most-negative first), lo = j; Bland: hi = 0,
 // lo = j. The minimum key is the same candidate block_reduce_cand /
 // block_reduce_pp pick (a total order, so the reduction tree cannot change
-// the winner). Within a wave: four DPP steps (xor 1, xor 2, half-mirror,
-// mirror) leave each 16-lane row's minimum in every lane of the row, then
-// the four rows through readlane; the winning lane is found by ballot and
-// its payload read with readlane; the four waves meet in LDS (one barrier
-// pair instead of log2(64) LDS permutes per field).
-
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
-}
+// the winner). Within a wave: the minimum hi by six DPP steps (xor 1, xor 2,
+// half-mirror, mirror within each 16-lane row, then row_bcast:15 and
+// row_bcast:31 across rows; lane 63 ends with it), lo only where several
+// lanes share that hi; the winning lane is found by ballot and its payload
+// read with readlane; the four waves meet in LDS through their keys (one
+// barrier, plus a leading one for callers that need it). Round 1's form
+// (16-lane rows by DPP on the full 96-bit key, then the rows by readlane)
+// took 1.16 / 0.90 us per pricing / ratio argmin in k_pivot_block
+// (profiles/r02_block_probe_fine*_before.log).
 
 __device__ __forceinline__ bool key_less(uint64_t ah, uint32_t al, uint64_t bh, uint32_t bl) {
     return ah < bh || (ah == bh && al < bl);
-}
-
-template <int CTRL>
-__device__ __forceinline__ void key_step(uint64_t &h, uint32_t &l) {
-    const uint32_t h0 = dpp32<CTRL>((uint32_t)h), h1 = dpp32<CTRL>((uint32_t)(h >> 32)), l1 = dpp32<CTRL>(l);
-    const uint64_t oh = ((uint64_t)h1 << 32) | h0;
-    if (key_less(oh, l1, h, l)) {
-        h = oh;
-        l = l1;
-    }
 }
 
 __device__ __forceinline__ uint32_t rdl32(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, lane); }
@@ -127,25 +116,42 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, int lane) {
     return ((uint64_t)rdl32((uint32_t)(v >> 32), lane) << 32) | rdl32((uint32_t)v, lane);
 }
 
-// minimum key of the wave, uniform in every lane
+// 64-bit DPP move: lanes outside ROWMASK's rows keep their own value
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)v, (int)(uint32_t)v, CTRL, ROWMASK, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(v >> 32), (int)(uint32_t)(v >> 32), CTRL,
+                                                               ROWMASK, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t min64(uint64_t a, uint64_t b) { return b < a ? b : a; }
+
+// minimum over the wave, in lane 63: four steps within each 16-lane row,
+// then row_bcast:15 (rows 1, 3 take lane 15 of the row below) and
+// row_bcast:31 (rows 2, 3 take lane 31)
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t m) {
+    m = min64(m, dpp64<0xB1>(m));          // quad_perm [1,0,3,2]: lane ^ 1
+    m = min64(m, dpp64<0x4E>(m));          // quad_perm [2,3,0,1]: lane ^ 2
+    m = min64(m, dpp64<0x141>(m));         // row_half_mirror
+    m = min64(m, dpp64<0x140>(m));         // row_mirror
+    m = min64(m, dpp64<0x142, 0xA>(m));    // row_bcast:15
+    m = min64(m, dpp64<0x143, 0xC>(m));    // row_bcast:31
+    return rdl64(m, 63);
+}
+
+// minimum key (h, l) of the wave, uniform in every lane: the minimum h
+// first, then -- only when several lanes hold it -- the minimum l among them
 __device__ __forceinline__ void wave_min_key(uint64_t &h, uint32_t &l) {
-    key_step<0xB1>(h, l);    // quad_perm [1,0,3,2]: lane ^ 1
-    key_step<0x4E>(h, l);    // quad_perm [2,3,0,1]: lane ^ 2
-    key_step<0x141>(h, l);   // row_half_mirror: i <-> 7 - i
-    key_step<0x140>(h, l);   // row_mirror: i <-> 15 - i
-    uint64_t bh = rdl64(h, 0);
-    uint32_t bl = rdl32(l, 0);
-#pragma unroll
-    for (int r = 1; r < 4; r++) {
-        const uint64_t rh = rdl64(h, 16 * r);
-        const uint32_t rl = rdl32(l, 16 * r);
-        if (key_less(rh, rl, bh, bl)) {
-            bh = rh;
-            bl = rl;
-        }
+    const uint64_t hm = wave_min_u64(h);
+    const unsigned long long tie = __ballot(h == hm);
+    uint32_t lm;
+    if (__popcll(tie) == 1) {
+        lm = rdl32(l, __ffsll((long long)tie) - 1);
+    } else {
+        lm = (uint32_t)wave_min_u64(h == hm ? (uint64_t)l : ~0ull);
     }
-    h = bh;
-    l = bl;
+    h = hm;
+    l = lm;
 }
 
 __device__ __forceinline__ int winner_lane(bool mine) {
@@ -154,8 +160,9 @@ __device__ __forceinline__ int winner_lane(bool mine) {
 }
 
 // == block_reduce_cand for candidates with theta >= 0 and unique keys
-// (NW waves per block; NW == 1: no LDS, no barrier)
-template <int NW = kBlock / 64>
+// (NW waves per block; NW == 1: no LDS, no barrier). LEAD: a barrier first,
+// for callers that may still be reading the previous call's exchange.
+template <int NW = kBlock / 64, bool LEAD = true>
 __device__ Cand block_argmin_cand(const Cand &c) {
     const bool valid = c.row >= 0;
     uint64_t h = valid ? (uint64_t)__double_as_longlong(c.theta) : ~0ull;
@@ -173,19 +180,31 @@ __device__ Cand block_argmin_cand(const Cand &c) {
     }
     if (NW == 1) return o;
     __shared__ Cand sw[NW];
+    __shared__ uint64_t sh[NW];
+    __shared__ uint32_t sl[NW];
     const int w = threadIdx.x >> 6;
+    if (LEAD) __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        sw[w] = o;
+        sh[w] = h;
+        sl[w] = l;
+    }
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) sw[w] = o;
-    __syncthreads();
-    Cand b = sw[0];
+    int bi = 0;
+    uint64_t bh = sh[0];
+    uint32_t bl = sl[0];
 #pragma unroll
     for (int i = 1; i < NW; i++)
-        if (cand_better(sw[i], b)) b = sw[i];
-    return b;
+        if (key_less(sh[i], sl[i], bh, bl)) {
+            bh = sh[i];
+            bl = sl[i];
+            bi = i;
+        }
+    return sw[bi];
 }
 
 // == block_reduce_pp<RULE> for eligible partials (v < 0, unique j)
-template <int RULE, int NW = kBlock / 64>
+template <int RULE, int NW = kBlock / 64, bool LEAD = true>
 __device__ PricePart block_argmin_pp(const PricePart &p) {
     const bool valid = p.j >= 0;
     uint64_t h = ~0ull;
@@ -207,15 +226,27 @@ __device__ PricePart block_argmin_pp(const PricePart &p) {
     }
     if (NW == 1) return o;
     __shared__ PricePart sw[NW];
+    __shared__ uint64_t sh[NW];
+    __shared__ uint32_t sl[NW];
     const int w = threadIdx.x >> 6;
+    if (LEAD) __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        sw[w] = o;
+        sh[w] = h;
+        sl[w] = l;
+    }
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) sw[w] = o;
-    __syncthreads();
-    PricePart b = sw[0];
+    int bi = 0;
+    uint64_t bh = sh[0];
+    uint32_t bl = sl[0];
 #pragma unroll
     for (int i = 1; i < NW; i++)
-        if (pp_better<RULE>(sw[i], b)) b = sw[i];
-    return b;
+        if (key_less(sh[i], sl[i], bh, bl)) {
+            bh = sh[i];
+            bl = sl[i];
+            bi = i;
+        }
+    return sw[bi];
 }
 
 // Pricing candidate of column j: dR is the (real)
