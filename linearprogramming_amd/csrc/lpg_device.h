@@ -139,17 +139,27 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t m) {
     return rdl64(m, 63);
 }
 
-// minimum key (h, l) of the wave, uniform in every lane: the minimum h
-// first, then -- only when several lanes hold it -- the minimum l among them
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ uint32_t dpp32m(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROWMASK, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t m) {
+    m = min(m, dpp32m<0xB1>(m));
+    m = min(m, dpp32m<0x4E>(m));
+    m = min(m, dpp32m<0x141>(m));
+    m = min(m, dpp32m<0x140>(m));
+    m = min(m, dpp32m<0x142, 0xA>(m));
+    m = min(m, dpp32m<0x143, 0xC>(m));
+    return rdl32(m, 63);
+}
+
+// minimum key (h, l) of the wave, uniform in every lane: the minimum h, then
+// the minimum l among the lanes holding it. Branch-free: a uniform branch
+// here made the compiler wait for the loads the callers keep in flight
+// across it (k_select_d's 64 multiplier loads: 10 -> 20 us per launch).
 __device__ __forceinline__ void wave_min_key(uint64_t &h, uint32_t &l) {
     const uint64_t hm = wave_min_u64(h);
-    const unsigned long long tie = __ballot(h == hm);
-    uint32_t lm;
-    if (__popcll(tie) == 1) {
-        lm = rdl32(l, __ffsll((long long)tie) - 1);
-    } else {
-        lm = (uint32_t)wave_min_u64(h == hm ? (uint64_t)l : ~0ull);
-    }
+    const uint32_t lm = wave_min_u32(h == hm ? l : ~0u);
     h = hm;
     l = lm;
 }

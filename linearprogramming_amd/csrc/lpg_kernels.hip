@@ -904,18 +904,26 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
     constexpr bool TWO = kPF > 64;
     static_assert(kPF <= 64 || kPF == 128, "prefetch slots");
     const int npf = D.q < B0 ? D.q : B0;
-    double cv[B0];                   // slots past the pending block: +0 (with P entries +0 below: no-op steps)
+    // slots past the pending block: +0 (with P entries +0 below: no-op steps).
+    // The loads are unconditional (a clamped address, then a select): a load
+    // behind a per-slot condition became a branch, and the compiler then
+    // waited for each load before issuing the next (64 round trips)
+    double cv[B0];
+    const int64_t ic = crow ? i : 0;
 #pragma unroll
     for (int u = 0; u < B0; u++) {
-        cv[u] = 0.0;
-        if (u < npf && crow) cv[u] = D.Cbuf[(int64_t)u * D.cs + i];
+        const double v = D.Cbuf[(int64_t)(u < npf ? u : 0) * D.cs + ic];
+        cv[u] = (u < npf && crow) ? v : 0.0;
     }
     double cv1[TWO ? 64 : 1];        // bank 1: slots 64 .. D.q - 1 (pivot t's own C_t is added below)
     const int npf1 = TWO && D.q > 64 ? D.q - 64 : 0;
 #pragma unroll
     for (int u = 0; u < (TWO ? 64 : 1); u++) {
         cv1[u] = 0.0;
-        if (TWO && u < npf1 && crow) cv1[u] = D.Cbuf[(int64_t)(64 + u) * D.cs + i];
+        if (TWO) {
+            const double v = D.Cbuf[(int64_t)(u < npf1 ? 64 + u : 0) * D.cs + ic];
+            cv1[u] = (u < npf1 && crow) ? v : 0.0;
+        }
     }
     // lane q of every wave holds P_q[0], r_q (q <= D.q: pivot t included);
     // bank 1 slot 64 + q in lane q
@@ -1951,6 +1959,10 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
     constexpr int MT = LM ? K * K / kBlock : 1;         // multipliers staged per thread
     __shared__ double sP[K][64];
     __shared__ __attribute__((aligned(32))) double sM[LM ? K * K : 4];   // [u][q]
+    // K = 128: each wave stages its group's multipliers mul[u][q0 .. q0 + 3]
+    // (4 KB) in its own LDS rows, all loads in flight at once (a uniform load
+    // per chain step would wait for each in turn)
+    __shared__ __attribute__((aligned(32))) double sMg[LM ? 1 : kBlock / 64][LM ? 1 : K][4];
     const int np = (int)st->npend;
     if (np <= 0) return;
     const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1984,8 +1996,16 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
         const int q0 = 4 * grp;
         if (q0 >= np) continue;                         // uniform
         double x0 = sP[q0][c], x1 = sP[q0 + 1][c], x2 = sP[q0 + 2][c], x3 = sP[q0 + 3][c];
+        if (!LM) {                                      // this wave's rows only: no barrier
+#pragma unroll
+            for (int k = 0; k < (LM ? 1 : K / 64); k++) {
+                const int u = c + 64 * k;
+                const d4 m = *(const d4 *)(mul + (u < np ? u : 0) * LPG_DEFER_MAX + q0);
+                *(d4 *)&sMg[LM ? 0 : w][LM ? 0 : u][0] = u < np ? m : d4{0.0, 0.0, 0.0, 0.0};
+            }
+        }
         auto m4 = [&](int u) {                          // mul[u][q0 .. q0 + 3]
-            return LM ? *(const d4 *)(sM + u * K + q0) : *(const d4 *)(mul + u * LPG_DEFER_MAX + q0);
+            return LM ? *(const d4 *)(sM + u * K + q0) : *(const d4 *)&sMg[LM ? 0 : w][LM ? 0 : u][0];
         };
         if (q0 + 1 < np) {
             const double p = sP[q0 + 1][c];
@@ -2070,9 +2090,11 @@ __global__ __launch_bounds__(kPlanNT) void k_swap_plan(const DevState *__restric
         const int64_t r = q < np ? rq[q] : -1;
         double v[UB];
 #pragma unroll
-        for (int k = 0; k < UB; k++) {
+        for (int k = 0; k < UB; k++) {   // unconditional loads (clamped address, then a select): all in flight
             const int u = u0 + k;
-            v[k] = (u > q && u < np && r >= 0) ? -Cbuf[(int64_t)u * cs + r] : 0.0;
+            const bool on = u > q && u < np && r >= 0;
+            const double c = Cbuf[(int64_t)(on ? u : 0) * cs + (on ? r : 0)];
+            v[k] = on ? -c : 0.0;
         }
 #pragma unroll
         for (int k = 0; k < UB; k++)
