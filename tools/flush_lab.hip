@@ -18,7 +18,10 @@
 // per SIMD cannot hide it. Two 16-row bands per step in k_flushw<128> (4
 // independent MFMA chains per wave instead of 2) is no faster either: 3.07 ms
 // (profiles/r02_flush_lab_k128_sb2.log), so the 1-wave issue stream, not the
-// chain latency, is the limit.
+// chain latency, is the limit. Reading the band's A operands 4-32 MFMA groups
+// ahead: 3.00-3.02 ms; 3- or 4-deep multiplier rings: 3.02-3.08 ms
+// (profiles/r02_flush_lab_k128_apre.log, _ring.log): the loop sits at ~46
+// TFLOP/s whatever feeds it.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o tools/flush_lab tools/flush_lab.hip
 //   tools/flush_lab [rows]            (LAB_ONLY=substring picks designs)
 #include "../linearprogramming_amd/csrc/lpg_kernels.hip"
@@ -481,6 +484,9 @@ int main(int argc, char **argv) {
 #define X(KM, SB, LB, R) \
     if (want("x<" #KM "," #SB "," #LB "," #R ">")) run(L, fn_x<KM, SB, LB, R>, "x<" #KM "," #SB "," #LB "," #R ">", reps);
     W(128, 2, 1, 512)
+    W(128, 3, 1, 512)
+    W(128, 4, 1, 512)
+    W(128, 3, 1, 1024)
     X(128, 2, 1, 512)
 #define Y(KM, LB, PF, R) \
     if (want("y<" #KM "," #LB "," #PF "," #R ">")) run(L, fn_y<KM, LB, PF, R>, "y<" #KM "," #LB "," #PF "," #R ">", reps);
