@@ -162,7 +162,11 @@ int  lpg_comm_init_host(lpg_ctx *ctx, const lpg_host_comm_ops *ops);
  * (lpg_comm_push_handle -> exchange -> lpg_comm_init_push), device pointers
  * between ranks of one process (lpg_comm_push_base -> lpg_comm_init_push_local).
  * Waits are bounded (2 s): a rank that waits longer ends the solve with
- * LPG_NUMERIC and lpg_last_error names the exchange. */
+ * LPG_NUMERIC and lpg_last_error names the exchange. With the push attached,
+ * blocks of <= 64 pivots run as one persistent launch per block on every
+ * rank (lpg_info.pivot_wg > 0; each rank needs its own GPU, or launches
+ * small enough to be resident together; env LPG_PERSIST_MR=0: two kernels
+ * per pivot). */
 #define LPG_PUSH_HANDLE_BYTES 64
 int  lpg_comm_push_handle(lpg_ctx *ctx, void *handle, size_t len);
 int  lpg_comm_push_base(lpg_ctx *ctx, void **base);

@@ -911,7 +911,7 @@ int lpg_comm_unique_id(void *uid, size_t len) {
 // With a communicator the deferred pair runs in 256-thread blocks (its
 // candidate count must match across ranks): drop a 128-thread choice.
 static void comm_pivot_blocks(lpg_ctx *c) {
-    if (c->persist) {                                  // the persistent kernel is single-rank only
+    if (c->persist) {   // the single-rank form; the multi-rank one comes with the push exchange (attach_push)
         c->persist = false;
         c->nsel_d = pivot_d_blocks(geo(c), 1, 256);    // <= the allocation (sized for max(nsel, nwg))
         c->booted = false;
