@@ -84,12 +84,18 @@ __host__ __device__ constexpr int slot_stride(int ks) { return ((ks + 15) & ~15)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, int bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, bytes, 0x00020000);
 }
-// ONE 16-byte write-through store / load (aux 16 = sc1)
+// ONE 16-byte write-through store / load (aux 16 = sc1; LPG_REC_*_AUX: experiments)
+#ifndef LPG_REC_ST_AUX
+#define LPG_REC_ST_AUX 16
+#endif
+#ifndef LPG_REC_LD_AUX
+#define LPG_REC_LD_AUX 16
+#endif
 __device__ __forceinline__ void rec_store(__amdgpu_buffer_rsrc_t r, int off, u4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, LPG_REC_ST_AUX);
 }
 __device__ __forceinline__ u4 rec_load(__amdgpu_buffer_rsrc_t r, int off) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, LPG_REC_LD_AUX);
 }
 // 8-byte write-through store / load of a double (global_store/load_dwordx2 sc1)
 __device__ __forceinline__ void st_wt(double *p, double v) {
