@@ -277,10 +277,13 @@ def main():
     use_push = use_push and eng.info.exchange > 0
     K = eng.info.defer_k or 1                           # pivots per step (one block; eager: one pivot)
     warm, timed = a.warmup * K, a.steps * K
-    eng.reserve_log(warm + timed + 8)
+    # the push exchange is proven on untimed pivots before the timed region:
+    # the warm-up, or one block of its own when --warmup 0
+    warm_run = warm if (warm > 0 or not use_push) else K
+    eng.reserve_log(warm_run + timed + 8)
     failed = 0
     try:
-        eng.enqueue(warm, lpg.RULE_DANTZIG)
+        eng.enqueue(warm_run, lpg.RULE_DANTZIG)
         before = eng.sync().pivots
     except lpg.LPGError as ex:                          # the push exchange did not work here: collectives instead
         if not use_push:
