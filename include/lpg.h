@@ -115,7 +115,9 @@ typedef struct {
                                    16 * (nrows + nobj) * ncols (one read + one write) */
     int32_t exchange;           /* per-pivot exchange of a multi-rank context: 0 collectives (or none),
                                    1 owner push, 2 owner push into uncached exchange buffers */
-    int32_t pad2_;
+    int32_t column_trade;       /* 1: the deferred path keeps the nonbasic columns contiguous (a column
+                                   trade at every block's end; default from 2 GB per single rank, env
+                                   LPG_NO_REORDER=0/1) */
 } lpg_info_t;
 
 typedef struct {

@@ -66,6 +66,7 @@ struct lpg_ctx {
     bool persist = false;         // single rank, no communicator: k_pivot_block
     bool pmr = false;             // k_pivot_block's geometry also holds for the multi-rank form (same on every rank)
     bool persist_x = false;       // multi-rank k_pivot_block over the owner-push exchange (attach_push)
+    bool no_reorder = false;      // LPG_NO_REORDER=1: keep the caller's column order (no block-end column trade)
     int pb_nwg = 0, pb_cw = 0, pb_rw = 0;
     size_t pb_lds = 0;
     void *rec = nullptr;          // its records (zeroed once; tags never repeat within a context)
@@ -313,7 +314,7 @@ static Defer defer_of(const lpg_ctx *c, int q) {
 // with a communicator k_price mode 1 between them prices logical keys): every
 // rank runs the same plan from replicated data (kq, lv, pv), so the physical
 // order, and with it the exchanged P, is the same on every rank.
-static bool reorders(const lpg_ctx *c) { return c->defer_k > 0 && c->fast_pivot && c->colmap; }
+static bool reorders(const lpg_ctx *c) { return c->defer_k > 0 && c->fast_pivot && c->colmap && !c->no_reorder; }
 
 // The timing ring brackets the block pass alone (k_flushw / k_flushm), the
 // kernel the roofline reports; the swap plan, pivot-row rewrite and column
@@ -792,6 +793,12 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         delete c;
         return LPG_ERR_ARG;
     }
+    // the block-end column trade (§3.3 of DESIGN.md) pays where the block pass
+    // is long; below 2 GB on one rank its kernels cost more than scattered
+    // live columns do (config 2: 105k -> 112k pivots/s without it, config 5:
+    // 67k -> 69k, config 3: 25k -> 21k). LPG_NO_REORDER=0/1 decides instead.
+    const char *nr = getenv("LPG_NO_REORDER");
+    c->no_reorder = nr ? atoi(nr) != 0 : (world == 1 && tbytes < 2e9);
     const char *sp = getenv("LPG_SLOW_PIVOT");
     c->fast_pivot = !(sp && atoi(sp));
     const char *fv = getenv("LPG_FLUSH_KERNEL");   // m | w: force k_flushm / k_flushw (tests); default by block size
@@ -1075,7 +1082,7 @@ int lpg_info(const lpg_ctx *c, lpg_info_t *o) {
     o->pivot_wg = ((c->persist && !has_comm(c)) || (c->persist_x && c->xmode)) ? c->pb_nwg : 0;
     o->bytes_per_pivot = 16.0 * (double)(c->nloc + c->nobj) * (double)c->ncols;
     o->exchange = c->xmode ? (c->xuncached ? 2 : 1) : 0;
-    o->pad2_ = 0;
+    o->column_trade = reorders(c) ? 1 : 0;
     return 0;
 }
 

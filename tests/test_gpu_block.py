@@ -73,11 +73,13 @@ def test_engaged_where_the_slices_fit(lpg, monkeypatch):
     assert _engine(lpg, monkeypatch, 8, 256 * 256 + 3, defer=8).info.pivot_wg == 0
 
 
+@pytest.mark.parametrize("trade", ["0", "1"])
 @pytest.mark.parametrize("wg", [None, 3, 7, 64, 256])
 @pytest.mark.parametrize("defer", [8, 32, 64])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(200, 300, 12, 0, 0), (48, 48, 14, 1, 1), (257, 100, 15, 1, 0)])
-def test_to_optimality(lpg, monkeypatch, wg, defer, m, n, seed, kind, rule):
+def test_to_optimality(lpg, monkeypatch, wg, defer, m, n, seed, kind, rule, trade):
     assert _fits(m, n + m + 1, defer, wg)
+    monkeypatch.setenv("LPG_NO_REORDER", "0" if trade == "1" else "1")
     e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer, wg=wg)
     assert e.info.pivot_wg > 0
     o = Oracle(m, n + m + 1)

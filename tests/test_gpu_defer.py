@@ -44,10 +44,15 @@ def _engine(lpg, monkeypatch, k, m, ncols, **kw):
     return e
 
 
+@pytest.mark.parametrize("trade", ["0", "1"])
 @pytest.mark.parametrize("k", [0, 1, 2, 3, 8, 16, 31, 32, 64, 65, 100, 128])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(200, 300, 12, 0, 0), (48, 48, 14, 1, 1), (257, 100, 15, 1, 0)])
-def test_block_sizes_to_optimality(lpg, monkeypatch, k, m, n, seed, kind, rule):
+def test_block_sizes_to_optimality(lpg, monkeypatch, k, m, n, seed, kind, rule, trade):
+    """Every block size, with the block-end column trade (trade 1, forced on
+    for these small tableaus) and without it (their default)."""
+    monkeypatch.setenv("LPG_NO_REORDER", "0" if trade == "1" else "1")
     e = _engine(lpg, monkeypatch, k, m, n + m + 1)
+    assert e.info.column_trade == (1 if trade == "1" and k > 0 else 0)
     o = Oracle(m, n + m + 1)
     e.generate(n, seed, kind)
     o.generate(n, seed, kind)
@@ -192,10 +197,12 @@ def test_generic_and_prefetching_pivot_kernels_agree(lpg, monkeypatch, k, m, n, 
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1), (600, 1100, 3, 0, 0)])
 def test_reordered_columns_to_optimality(lpg, monkeypatch, k, m, n, seed, kind, rule):
     """Whole solves over many blocks: after every block the columns are reordered
-    (DESIGN.md §3.3), the entering column's physical index travels in
-    PricePart.pad through every reduction, and everything must stay bitwise the
-    oracle's."""
+    (forced on, these tableaus are below its 2 GB default),
+    the entering column's physical index travels in PricePart.pad through
+    every reduction, and everything must stay bitwise the oracle's."""
+    monkeypatch.setenv("LPG_NO_REORDER", "0")
     e = _engine(lpg, monkeypatch, k, m, n + m + 1)
+    assert e.info.column_trade == 1
     o = Oracle(m, n + m + 1)
     e.generate(n, seed, kind)
     o.generate(n, seed, kind)
@@ -214,6 +221,7 @@ def test_wide_tableau_more_partials_than_threads(lpg, monkeypatch, k, rule, cap)
     through inv (config 4's shape). Bland's rule needs ~41k
     pivots here, so it stops at an iteration limit."""
     m, n = 96, 140_000
+    monkeypatch.setenv("LPG_NO_REORDER", "0")      # the physical column through inv (only with the trade)
     e = _engine(lpg, monkeypatch, k, m, n + m + 1)
     o = Oracle(m, n + m + 1, nthreads=8)
     e.generate(n, 7, 0)
