@@ -7,7 +7,7 @@ over the reduced-cost row) -> ratio test (min over the entering column) ->
 Gauss-Jordan rank-1 update of the whole tableau. The update is deferred:
 prep / select evaluate the pending chain for the entries they need and
 k_flushw applies each block of K pivots (LPG_DEFER; 128 for tableaus >= 16 GB
-per rank, 64 from 512 MB, else 32) to the constraint rows in one HBM pass,
+per rank, 64 from 200 MB, else 32) to the constraint rows in one HBM pass,
 bitwise identical to K eager updates.
 
 A "step" is one such block: K pivots and the one pass over the tableau that
@@ -168,8 +168,8 @@ def config5(a):
             "config": {"workload": cfg["name"], "m": m, "n": n, "rule": "bland", "art_first": art_first},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": ("lpg::k_flushw" if eng.info.defer_k > 32 else "lpg::k_flushm") if eng.info.defer_k
-                                   else "lpg::k_update",
+                         "kernel": ("lpg::" + ("k_flushw" if lpg.flush_kernel_for(eng.info.defer_k) == "w" else "k_flushm"))
+                                   if eng.info.defer_k else "lpg::k_update",
                          "launches_timed": timing.update_count,
                          "algorithmic_bytes_per_launch": touched,
                          "full_tableau_bytes_per_launch": eng.info.bytes_per_pivot, "update_ms_mean": upd_ms},

@@ -80,7 +80,7 @@ extern "C" {
 
 /* Deferred updates (default): the constraint rows are brought up to date in
  * one HBM pass per block of up to LPG_DEFER_MAX pivots (128 when a rank's
- * tableau is >= 16 GB, 64 when >= 512 MB, else 32; env LPG_DEFER=K picks K,
+ * tableau is >= 16 GB, 64 when >= 200 MB, else 32; env LPG_DEFER=K picks K,
  * K in 1 .. 128; 0 = eager; the persistent pivot kernel takes blocks of at
  * most 64). Values,
  * pivot sequence and log are bitwise those of eager updates; every call that

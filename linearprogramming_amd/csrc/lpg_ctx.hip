@@ -427,7 +427,7 @@ static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
 static constexpr int kGraphPivots = 32;
 static constexpr int kDefaultDeferHuge = 128;   // pivots per flush (LPG_DEFER), tableaus >= 16 GB per rank
 static constexpr int kDefaultDefer = 64;        // pivots per flush, large tableaus
-static constexpr int kDefaultDeferSmall = 32;   // tableaus below 512 MB per rank
+static constexpr int kDefaultDeferSmall = 32;   // tableaus below 200 MB per rank
 
 static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule);
 
@@ -777,15 +777,17 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     const char *ns = getenv("LPG_NO_SKIP");
     c->skip = ((flags & LPG_FLAG_NO_SKIP) || (ns && atoi(ns))) ? 0 : 1;
     const char *dk = getenv("LPG_DEFER");
-    // default block: 64 pivots once this rank's tableau is >= 512 MB (the
+    // default block: 64 pivots once this rank's tableau is >= 200 MB (the
     // flush dominates; k_flushw keeps 64-pivot flushes memory-bound), 32 below
-    // (the per-pivot chains dominate: config 2 runs 66k pivots/s at 32, 59k at 64)
+    // (the per-pivot work dominates: m = 2048, n = 4096 (100 MB) 100k pivots/s
+    // at 32, 99k at 64; m = 4096, n = 8192 (403 MB) 77k / 82k,
+    // profiles/r02_k32_64.log)
     const int64_t nloc_guess = m * (rank + 1) / world - m * rank / world;
     // 128 once it is >= 16 GB (too big for the persistent pivot kernel's
     // slices; the 128-pivot pass is ~10% cheaper per pivot than two 64-pivot
     // passes, tools/flush_lab.hip)
     const double tbytes = (double)nloc_guess * (double)ncols * 8.0;
-    const int kdef = tbytes >= 16e9 ? kDefaultDeferHuge : tbytes >= 512e6 ? kDefaultDefer : kDefaultDeferSmall;
+    const int kdef = tbytes >= 16e9 ? kDefaultDeferHuge : tbytes >= 200e6 ? kDefaultDefer : kDefaultDeferSmall;
     c->defer_k = (flags & LPG_FLAG_EAGER) ? 0 : (dk ? atoi(dk) : kdef);
     if (c->defer_k < 0 || c->defer_k > LPG_DEFER_MAX || (c->defer_k && !flush_kmax_supported(c->defer_k))) {
         fail(c, LPG_ERR_ARG, "LPG_DEFER=%d out of range [0, %d]", c->defer_k, LPG_DEFER_MAX);

@@ -2316,12 +2316,14 @@ int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, in
     return rc ? rc : launch_flush_tail(L, g, st, D, kmax);
 }
 
-// which: -1 = default (k_flushm for blocks of <= 32 pivots, k_flushw for 64),
-// 0 = k_flushm, 1 = k_flushw (LPG_FLUSH_KERNEL=m|w, tests). Both bitwise.
+// which: -1 = default (k_flushw), 0 = k_flushm (blocks of <= 32 pivots),
+// 1 = k_flushw (LPG_FLUSH_KERNEL=m|w, tests). Both bitwise.
 int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which) {
     kmax = flush_kmax_supported(kmax);
     if (!kmax) return -1;
-    if (which < 0) which = kmax >= 64 ? 1 : 0;
+    // k_flushw by default at every block size: at 32 slots too it beats
+    // k_flushm by 3-4% (m = 1024 .. 4096, profiles/r02_k32_flush.log)
+    if (which < 0) which = 1;
     if (kmax >= 64) which = 1;                              // k_flushm's C tile caps it at 32 slots
     hipStream_t stream = (hipStream_t)L.stream;
     if (which == 1) {

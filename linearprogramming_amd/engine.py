@@ -57,9 +57,9 @@ def _stdout_to_stderr():
 
 def flush_kernel_for(pending: int) -> str:
     """Which block-pass kernel the default configuration launches for `pending`
-    pivots (lpg_kernels.hip launch_flush_main): "w" = k_flushw (64- and
-    128-slot blocks), "m" = k_flushm (<= 32 slots)."""
-    return "w" if pending > 32 else "m"
+    pivots (lpg_kernels.hip launch_flush_main): k_flushw at every block size
+    ("m" = k_flushm only when LPG_FLUSH_KERNEL=m asks for it, <= 32 slots)."""
+    return "w"
 
 
 def device_count() -> int:

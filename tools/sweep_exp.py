@@ -12,7 +12,7 @@ import linearprogramming_amd as lpg  # noqa: E402
 
 if len(sys.argv) > 1:
     lpg.load(sys.argv[1])
-m, n = 16384, 32768
+m, n = int(os.environ.get("M", 16384)), int(os.environ.get("N", 32768))
 e = lpg.Engine(m, n + m + 1)
 e.generate(n, 20220518, 0)
 K = e.info.defer_k
@@ -23,5 +23,6 @@ t0 = time.perf_counter()
 e.enqueue(32 * K, 0)
 r = e.sync()
 dt = time.perf_counter() - t0
-print(f"{os.path.basename(sys.argv[1]) if len(sys.argv) > 1 else 'liblpg.so'}: {32 * K / dt:.0f} pivots/s, "
+print(f"{os.path.basename(sys.argv[1]) if len(sys.argv) > 1 else 'liblpg.so'} m={m} n={n} K={K} "
+      f"flush={os.environ.get('LPG_FLUSH_KERNEL', 'default')}: {32 * K / dt:.0f} pivots/s, "
       f"{dt / 32 * 1e3:.3f} ms/block, pivots {r.pivots}")
