@@ -1,0 +1,229 @@
+"""The host front end (linearprogramming_amd/frontend.py): LP text -> the
+reference's SimplexMatrix, checked against the reference itself.
+
+* the 12 fixture LPs: equal to tests/golden/kat_cases.json, the tableaus read
+  back from the reference binary's transcripts (tests/golden/make_golden.py);
+* 200 random LPs in the reference's format (free and x <= 0 variables, min and
+  max, objective constants, decimals, fractions, negative right-hand sides,
+  terms on either side, =, >=, <= rows): equal to what the reference binary
+  (oracle/_ref/lp, compiled from /root/reference by oracle/Makefile) prints
+  after LPAlign -- or rejected by both. Skipped where that binary is absent
+  (the GPU box builds nothing; the CPU suite runs here);
+* on the GPU: the device solve of the fixture LPs (known optima, Appendix A)
+  and of random LPs against HiGHS on the same SimplexMatrix.
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+import subprocess
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+import refparse
+
+from linearprogramming_amd import frontend as F
+
+LP = os.path.join(ROOT, "tests", "golden", "lp")
+REF = os.path.join(ROOT, "oracle", "_ref", "lp")
+needs_ref = pytest.mark.skipif(not os.path.exists(REF), reason="oracle/_ref/lp not built (needs /root/reference)")
+
+
+def _fx(s):
+    return Fraction(s)
+
+
+def _as_case(sm: F.SMatrix):
+    return {"names": sm.display_names, "basis": sm.basis, "lacking": sm.lacking, "costs": sm.costs,
+            "constant": sm.constant, "zcoef": sm.zcoef, "rows": sm.rows}
+
+
+def _same(sm: F.SMatrix, names, basis, lacking, costs, constant, zcoef, rows):
+    got = _as_case(sm)
+    exp = {"names": names, "basis": basis, "lacking": lacking, "costs": costs, "constant": constant,
+           "zcoef": zcoef, "rows": rows}
+    return got == exp, got, exp
+
+
+@pytest.mark.parametrize("case", json.load(open(os.path.join(ROOT, "tests", "golden", "kat_cases.json"))),
+                         ids=lambda c: c["name"])
+def test_fixture_lps_build_the_reference_smatrix(case):
+    sm = F.build_smatrix(open(os.path.join(LP, case["name"])).read())
+    ok, got, exp = _same(sm, case["names"], case["basis"], case["lacking"], [_fx(c) for c in case["costs"]],
+                         _fx(case["constant"]), _fx(case["zcoef"]), [[_fx(x) for x in r] for r in case["rows"]])
+    assert ok, (got, exp)
+
+
+def test_shipped_testdata_is_rejected_like_the_reference():
+    """The reference's own testdata.txt writes `ma:` (dataReader.c:455): not a model."""
+    with pytest.raises(F.FrontendError, match="Objective function invalid"):
+        F.build_smatrix(open(os.path.join(LP, "testdata_shipped.txt")).read())
+
+
+def test_decimal_truncation_and_gcd_quirks():
+    """Fractionize's (long)(d * 10^k) truncation (basicFuncs.c:264) and
+    FormulaSimplify's separate numerator / denominator GCDs (dataReader.c:409-428)."""
+    assert F.fractionize("0.29") == Fraction(28, 100)          # 0.29 * 100 = 28.999...
+    assert F.fractionize("-2.45") == Fraction(-49, 20)
+    assert F.fractionize("0/5") is None and F.fractionize(".5") is None
+    f = F._formula("2x1+4x2<=6")
+    assert [t.coef for t in f.left] == [1, 2] and f.right[0].coef == 3
+    f = F._formula("1/2x1+1/4x2<=1/2")
+    assert [t.coef for t in f.left] == [1, Fraction(1, 2)] and f.right[0].coef == 1
+
+
+def test_sign_constraint_before_use_makes_the_variable_free():
+    """PutVarItem replaces (hashTable.c): a later constraint re-registers x1 as
+    unrestricted, so `x1>=0` written first is lost: x1 = x3 - x4 (the reference
+    binary prints the same columns x2 x3 x4 x5)."""
+    sm = F.build_smatrix("OF {\n max:z=x1+x2\n}\nST {\n x1>=0;\n x1+x2<=4;\n x2>=0\n}\n")
+    assert sm.names == ["x2", "x3", "x4", "x5"]
+    it = sm.vars.items["x1"]
+    assert it.relation == 0 and (it.former, it.latter) == ("x3", "x4")
+
+
+def _rand_coef(rng, v):
+    return rng.choice([str(v), f"{v}/{rng.integers(2, 9)}", f"{v}.{rng.integers(1, 99)}"])
+
+
+def _random_lp_rich(rng):
+    """A random model in the reference's format, exercising its standardisation."""
+    n = int(rng.integers(1, 6))
+    m = int(rng.integers(1, 5))
+    signs = [rng.choice(["ge", "le", "free"], p=[0.6, 0.2, 0.2]) for _ in range(n)]
+    if not any(s != "free" for s in signs):
+        signs[0] = "ge"
+
+    def expr(allow_const=False):
+        terms = []
+        for j in range(1, n + 1):
+            if rng.random() < 0.75:
+                v = int(rng.integers(1, 9))
+                terms.append(("-" if rng.random() < 0.25 else "+") + _rand_coef(rng, v) + f"x{j}")
+        if not terms:
+            terms = [f"+x{int(rng.integers(1, n + 1))}"]
+        if allow_const and rng.random() < 0.3:
+            terms.append("+" + _rand_coef(rng, int(rng.integers(1, 9))))
+        e = "".join(terms)
+        return e[1:] if e[0] == "+" else e
+
+    rows = []
+    for _ in range(m):
+        rel = rng.choice(["<=", ">=", "="], p=[0.6, 0.25, 0.15])
+        rhs = int(rng.integers(-5, 40))
+        if rng.random() < 0.15:                       # a variable moved to the right-hand side
+            rows.append(f"{expr()}{rel}{rhs}+x{int(rng.integers(1, n + 1))}")
+        else:
+            rows.append(f"{expr()}{rel}{rhs}")
+    used = set(int(v) for r in rows for v in re.findall(r"x(\d+)", r))
+    for j in range(1, n + 1):                          # every variable appears in a constraint
+        if j not in used:
+            rows.append(f"x{j}<=30")
+    for j, s in enumerate(signs, 1):
+        if s == "ge":
+            rows.append(f"x{j}>=0")
+        elif s == "le":
+            rows.append(f"x{j}<=0")
+    obj_terms = "+".join(f"{_rand_coef(rng, int(rng.integers(1, 9)))}x{j}" for j in range(1, n + 1))
+    if rng.random() < 0.3:
+        obj_terms += "+" + _rand_coef(rng, int(rng.integers(1, 9)))
+    obj = f"{rng.choice(['max', 'min'])}:z={obj_terms}"
+    return "OF {\n\t" + obj + "\n}\nST {\n\t" + ";\n\t".join(rows) + "\n}\n"
+
+
+def _reference_aligned(path):
+    """The reference binary's tableau after LPAlign; None if it rejected the
+    model, "crash" if it died first (heap corruption in its term arrays on some
+    models with free variables: `realloc(): invalid next size`)."""
+    p = subprocess.run([REF, path], input="\n1\n\n\n1\n\n\nq\n", capture_output=True, text=True, timeout=20,
+                       cwd=ROOT, env={"TERM": "dumb", "PATH": "/usr/bin:/bin"})
+    models = refparse.parse_models(p.stdout)
+    if len(models) < 3:
+        return "crash" if p.returncode < 0 else None
+    return refparse.tableau_from_aligned(models[2])
+
+
+@needs_ref
+def test_random_lps_match_the_reference_binary(tmp_path):
+    rng = np.random.default_rng(20220607)
+    compared = rejected = crashed = 0
+    for t in range(200):
+        text = _random_lp_rich(rng)
+        f = tmp_path / f"r{t}.txt"
+        f.write_text(text)
+        rt = _reference_aligned(str(f))
+        if rt == "crash":                 # nothing to compare with
+            crashed += 1
+            continue
+        if rt is None:
+            with pytest.raises(F.FrontendError):
+                F.build_smatrix(text)
+            rejected += 1
+            continue
+        sm = F.build_smatrix(text)
+        ok, got, exp = _same(sm, rt.names, rt.basis, rt.lacking, rt.costs, rt.constant, rt.zcoef, rt.T)
+        assert ok, (text, got, exp)
+        compared += 1
+    assert compared >= 150, (compared, rejected, crashed)
+
+
+# ---- device solve ------------------------------------------------------------
+
+KNOWN = [("testdata_max.txt", 12.0), ("kat_wyndor.txt", 36.0), ("kat_min_ge.txt", -20.0),
+         ("a6_decimals.txt", 194 / 25), ("kat_negative_rhs.txt", 18.0), ("a5_lack_row.txt", 6.0),
+         ("a7_identity_quirk.txt", 2.0), ("a3_min_eq_neg.txt", 31 / 3)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["two_phase", "big_m"])
+@pytest.mark.parametrize("name,z", KNOWN)
+def test_device_solve_of_fixture_lps(lpg, name, z, method):
+    sol = F.solve_text(open(os.path.join(LP, name)).read(), method=method)
+    assert sol.status == "OPTIMAL"
+    assert abs(sol.z - z) < 1e-9 * max(1.0, abs(z))
+
+
+@pytest.mark.gpu
+def test_device_solve_readout(lpg):
+    """Appendix A2 (x1 = 0, x2 = 17/3, slack x4 = 6); A3 (x3 <= 0 un-substituted)."""
+    sol = F.solve_text(open(os.path.join(LP, "testdata_max.txt")).read())
+    assert sol.variables["x1"] == 0.0 and abs(sol.variables["x2"] - 17 / 3) < 1e-12
+    assert abs(sol.columns["x4"] - 6.0) < 1e-12
+    sol = F.solve_text(open(os.path.join(LP, "a3_min_eq_neg.txt")).read())
+    assert abs(sol.variables["x1"] - 5 / 3) < 1e-12 and abs(sol.variables["x2"] - 7 / 3) < 1e-12
+    assert sol.variables["x3"] == 0.0
+    assert F.solve_text(open(os.path.join(LP, "kat_unbounded.txt")).read()).status == "UNBOUNDED"
+    assert F.solve_text(open(os.path.join(LP, "a4_free_var.txt")).read()).status == "UNBOUNDED"
+
+
+@pytest.mark.gpu
+def test_device_solve_of_random_lps_matches_highs(lpg, tmp_path):
+    from scipy.optimize import linprog
+    rng = np.random.default_rng(31)
+    solved = 0
+    for t in range(60):
+        text = _random_lp_rich(rng)
+        try:
+            sm = F.build_smatrix(text)
+        except F.FrontendError:
+            continue
+        A = np.array([[F._dec(x) for x in r[1:]] for r in sm.rows])
+        b = np.array([F._dec(r[0]) for r in sm.rows])
+        c = np.array([F._dec(x) for x in sm.costs])
+        ref = linprog(-c, A_eq=A, b_eq=b, bounds=[(0, None)] * len(c), method="highs")
+        for method in ("two_phase", "big_m"):
+            sol = F.solve(sm, method=method)
+            if ref.status == 2:
+                assert sol.status == "INFEASIBLE", (text, method, sol)
+            elif ref.status == 3:
+                assert sol.status == "UNBOUNDED", (text, method, sol)
+            else:
+                assert ref.status == 0 and sol.status == "OPTIMAL", (text, method, sol, ref.status)
+                zref = (-ref.fun + F._dec(sm.constant)) / F._dec(sm.zcoef)
+                assert abs(sol.z - zref) < 1e-7 * max(1.0, abs(zref)), (text, method, sol.z, zref)
+        solved += 1
+    assert solved >= 40
