@@ -589,3 +589,32 @@ def solve(sm: SMatrix, method: str = "two_phase", rule=None, device: int = 0) ->
 def solve_text(text: str, method: str = "two_phase", rule=None, device: int = 0) -> LPSolution:
     """LP text (the reference's input format) -> the optimum on the device."""
     return solve(build_smatrix(text), method=method, rule=rule, device=device)
+
+
+def main(argv=None) -> int:
+    """``python -m linearprogramming_amd.frontend model.txt [--big-m] [--bland]``:
+    the reference's input file solved on the device, non-interactively."""
+    import argparse
+    from . import _lib as L
+    ap = argparse.ArgumentParser(description=main.__doc__)
+    ap.add_argument("path")
+    ap.add_argument("--big-m", action="store_true", help="artificials by Big-M instead of two-phase")
+    ap.add_argument("--bland", action="store_true", help="Bland's rule instead of Dantzig's")
+    a = ap.parse_args(argv)
+    try:
+        sm = build_smatrix(open(a.path, "rb").read())
+    except FrontendError as ex:
+        print(ex)
+        return 2
+    sol = solve(sm, method="big_m" if a.big_m else "two_phase",
+                rule=L.RULE_BLAND if a.bland else L.RULE_DANTZIG)
+    print(f"{sol.status} after {sol.pivots} pivots ({sol.method})")
+    if sol.status == "OPTIMAL":
+        print(f"\tz = {sol.z:.12g}")
+        print("\t" + "".join(f"{k}={v:.12g} | " for k, v in sol.columns.items()))
+        print("Variables:\n\t" + "".join(f"{k}={v:.12g} | " for k, v in sol.variables.items()))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

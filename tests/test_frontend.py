@@ -173,6 +173,13 @@ def test_random_lps_match_the_reference_binary(tmp_path):
 
 # ---- device solve ------------------------------------------------------------
 
+@pytest.fixture(scope="module")
+def lpg():
+    import linearprogramming_amd as lpg
+    lpg.load()
+    return lpg
+
+
 KNOWN = [("testdata_max.txt", 12.0), ("kat_wyndor.txt", 36.0), ("kat_min_ge.txt", -20.0),
          ("a6_decimals.txt", 194 / 25), ("kat_negative_rhs.txt", 18.0), ("a5_lack_row.txt", 6.0),
          ("a7_identity_quirk.txt", 2.0), ("a3_min_eq_neg.txt", 31 / 3)]
