@@ -1376,8 +1376,12 @@ int lpg_solve_big_m(lpg_ctx *c, int64_t art_first, const double *cost, int64_t m
         return rc;
     lpg_result r;
     if ((rc = lpg_solve(c, max_pivots, rule, &r))) return rc;
-    if (r.status == LPG_OPTIMAL) {
-        // artificials still positive (M-part objective < 0) -> infeasible
+    if (r.status == LPG_OPTIMAL || r.status == LPG_UNBOUNDED) {
+        // artificials still positive (M-part objective < 0) -> infeasible; also
+        // at UNBOUNDED: the pricing takes a negative M part first and such a
+        // column is never a ray (every basic artificial would grow along it),
+        // so a ray found while the M objective is negative cannot reach
+        // feasibility (as oracle/lpo.c lpo_solve_big_m)
         double zM = 0, bsum = 0;
         std::vector<double> xb(c->nloc);
         if ((rc = lpg_get_rows(c, c->m, 1, row.data(), c->ncols)) || (rc = lpg_get_column0(c, xb.data()))) return rc;

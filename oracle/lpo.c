@@ -440,7 +440,11 @@ int lpo_solve_big_m(lpo_ctx *c, int64_t art_first, const double *cost, int64_t m
     free(cr); free(cm);
     lpo_result r;
     lpo_solve(c, max_pivots, rule, 1, &r);
-    if (r.status == LPO_OPTIMAL) {
+    /* artificials still positive -> infeasible; also at UNBOUNDED: the pricing
+     * takes a negative M part first, and such a column is never a ray (every
+     * basic artificial would grow along it), so a ray found while the M
+     * objective is still negative leaves the artificials positive for good */
+    if (r.status == LPO_OPTIMAL || r.status == LPO_UNBOUNDED) {
         double bsum = 0;
         for (int64_t i = 0; i < c->m; i++) bsum += fabs(c->T[i * c->ld]);
         if (c->T[c->m * c->ld] < -1e-9 * (bsum > 1.0 ? bsum : 1.0)) r.status = LPO_INFEASIBLE;

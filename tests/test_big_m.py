@@ -17,6 +17,9 @@ from util import STATUS
 # A5: max x1 + 2 x2; x1 + x2 = 3; x1 - x2 <= 1
 A5 = np.array([[3.0, 1, 1, 0, 1], [1.0, 1, -1, 1, 0], [0, 0, 0, 0, 0], [0, 0, 0, 0, 0]])
 INF = np.array([[2.0, 1, 1, 0, 1], [1.0, 1, 1, 1, 0], [0, 0, 0, 0, 0], [0, 0, 0, 0, 0]])
+# max x1; x2 = 1, x2 = 2 (artificials a1, a2): infeasible, and x1's column (0, 0)
+# is a ray of the real objective once the M part is optimal (a2 = 1 left)
+INF_RAY = np.array([[1.0, 0, 1, 1, 0], [2.0, 0, 1, 0, 1], [0, 0, 0, 0, 0], [0, 0, 0, 0, 0]])
 
 
 def _oracle(T, basis):
@@ -37,6 +40,12 @@ def test_a5_big_m(rule):
 def test_big_m_infeasible():
     o = _oracle(INF, [4, 3])
     assert o.solve_big_m(4, [1.0, 1.0, 0.0, 0.0], 100).status == STATUS["INFEASIBLE"]
+
+
+def test_big_m_infeasible_with_a_ray():
+    """A ray found while an artificial is still positive is INFEASIBLE, not UNBOUNDED."""
+    o = _oracle(INF_RAY, [3, 4])
+    assert o.solve_big_m(3, [1.0, 0.0, 0.0, 0.0], 100).status == STATUS["INFEASIBLE"]
 
 
 @pytest.mark.parametrize("m,n,rule", [(8, 8, RULE_BLAND), (33, 33, RULE_DANTZIG), (64, 64, RULE_BLAND)])
@@ -97,3 +106,11 @@ def test_gpu_big_m_bitwise(lpg, m, n, rule):
     ro = o.solve_big_m(art_first, None, 100_000, rule)
     assert r.status == ro.status and r.pivots == ro.pivots and r.objective == ro.objective
     _same(e, o, m + 2)
+
+
+@pytest.mark.gpu
+def test_big_m_infeasible_with_a_ray_on_device(lpg):
+    e = lpg.Engine(2, 5, flags=lpg._lib.FLAG_BIG_M)
+    e.load_tableau(INF_RAY, [3, 4])
+    assert e.solve_big_m(3, [1.0, 0.0, 0.0, 0.0], 100).status == STATUS["INFEASIBLE"]
+    e.close()
