@@ -13,8 +13,8 @@ all: $(LIB) host/lpgcli oracle
 $(LIB): $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h include/lpg.h
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_ctx.hip -ldl
 
-host/lpgcli: host/lpgcli.c include/lpg.h $(LIB)
-	$(CC) -O2 -std=c11 -Wall -Wextra -Iinclude -o $@ host/lpgcli.c -L$(dir $(LIB)) -llpg -Wl,-rpath,'$$ORIGIN/../linearprogramming_amd' -lm
+host/lpgcli: host/lpgcli.c host/lpfront.c host/lpfront.h include/lpg.h $(LIB)
+	$(CC) -O2 -std=c11 -Wall -Wextra -Iinclude -o $@ host/lpgcli.c host/lpfront.c -L$(dir $(LIB)) -llpg -Wl,-rpath,'$$ORIGIN/../linearprogramming_amd' -lm
 
 oracle:
 	$(MAKE) -C oracle

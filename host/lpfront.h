@@ -1,0 +1,66 @@
+/*
+ * lpfront.h — the reference's front end restated in plain C (host side).
+ *
+ * Model text in the reference's input format -> the SimplexMatrix the
+ * reference's CreateSMatrix builds (Source/matrix.c:19-91), as exact int64
+ * rationals: Parser / FormulaParser / FormulaSimplify (dataReader.c:148-498),
+ * LPTrans (dataReader.c:45-140), LPStandardize / LPAlign (simplex.c:91-354),
+ * CreateSMatrix with its lack list written correctly (the reference writes it
+ * through *lack[p++] and crashes on two or more lacking rows, matrix.c:86).
+ * The same restatement as linearprogramming_amd/frontend.py;
+ * tests/test_frontend.py checks the two agree on every fixture and 200
+ * random models. lpf_solve runs the result on the device through lpg.h.
+ */
+#ifndef LPFRONT_H
+#define LPFRONT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    int64_t num, den;            /* den > 0 */
+} lpf_q;
+
+typedef struct {
+    char name[24];
+    int relation;                /* 0 unrestricted, +-2 sign constraint / slack */
+    char former[24], latter[24]; /* x = former - latter for an unrestricted x */
+} lpf_var;
+
+typedef struct {
+    int64_t m, n;                /* rows, columns (b excluded) */
+    char (*names)[24];           /* n column variables (no prime) */
+    unsigned char *inverted;     /* x <= 0 columns (x' = -x) */
+    lpf_q *costs;                /* n, max form */
+    lpf_q *rows;                 /* m x (n + 1): b, a_i1 .. a_in */
+    int64_t *basis;              /* m: 1-based basic column by the identity heuristic, 0 = lacking */
+    lpf_q constant, zcoef;       /* objective constant dropped; -1 for a min */
+    lpf_var *vars;               /* the variable table, GetVarItems order */
+    int64_t nvars;
+} lpf_smatrix;
+
+/* 0 on success; otherwise -1 and the reference's message in err. */
+int lpf_build(const char *text, lpf_smatrix *out, char *err, size_t errlen);
+void lpf_free(lpf_smatrix *sm);
+
+typedef struct {
+    int status;                  /* lpg status */
+    int64_t pivots;
+    double z;                    /* original objective (constant added, min sign restored) */
+    double *x;                   /* n column values */
+    double *vals;                /* nvars user-variable values (un-substituted) */
+} lpf_solution;
+
+/* Device solve as the bridge does it: artificials for rows without a true unit
+ * column, two-phase (bigm = 0) or Big-M (bigm = 1). 0 on success. */
+int lpf_solve(const lpf_smatrix *sm, int bigm, int rule, int device, lpf_solution *out, char *err, size_t errlen);
+void lpf_solution_free(lpf_solution *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -10,6 +10,9 @@
  *   lpgcli --synthetic M N [--seed S] [--kind dense|degenerate]
  *          [--rule dantzig|bland] [--pivots K] [--device D]
  *   lpgcli --tableau FILE [--rule ...] [--pivots K]
+ *   lpgcli --lp MODEL [--big-m] [--rule ...]     the reference's model format,
+ *          through the C front end (lpfront.c) onto the device
+ *   lpgcli --lp-dump MODEL                       the SimplexMatrix as JSON (no device)
  *
  * FILE: "m ncols" then m+1 rows of ncols numbers ([b | a_1..a_N], objective
  * row last, d_j = z_j - c_j), then m basic columns (1-based).
@@ -21,6 +24,7 @@
 #include <string.h>
 #include <time.h>
 
+#include "lpfront.h"
 #include "lpg.h"
 
 static double now(void) {
@@ -39,6 +43,86 @@ static int usage(const char *argv0) {
                     " [--pivots K] [--device D]\n\t%s --tableau FILE [--rule dantzig|bland] [--pivots K]\n",
             argv0, argv0);
     return 2;
+}
+
+static char *read_all(const char *path) {
+    FILE *f = fopen(path, "rb");
+    if (!f) {
+        printf("File not readable or does not exist.\n");   /* main.c:41 wording */
+        return NULL;
+    }
+    size_t cap = 4096, n = 0;
+    char *b = (char *)malloc(cap);
+    for (size_t r; b && (r = fread(b + n, 1, cap - n - 1, f)) > 0;) {
+        n += r;
+        if (n + 1 == cap) b = (char *)realloc(b, cap *= 2);
+    }
+    fclose(f);
+    if (b) b[n] = '\0';
+    return b;
+}
+
+static void print_q(lpf_q q) { printf("\"%lld/%lld\"", (long long)q.num, (long long)q.den); }
+
+/* the reference model file -> SimplexMatrix (dump) or the device optimum */
+static int run_lp(const char *path, int dump, int bigm, int rule, int device) {
+    char err[512] = "";
+    char *text = read_all(path);
+    if (!text) return 1;
+    lpf_smatrix sm;
+    const int rc = lpf_build(text, &sm, err, sizeof err);
+    free(text);
+    if (rc) {
+        printf("{\"error\": \"%s\"}\n", err);
+        return 3;
+    }
+    if (dump) {
+        printf("{\"names\": [");
+        for (int64_t j = 0; j < sm.n; j++) printf("%s\"%s%s\"", j ? ", " : "", sm.names[j], sm.inverted[j] ? "'" : "");
+        printf("], \"basis\": [");
+        for (int64_t i = 0; i < sm.m; i++) printf("%s%lld", i ? ", " : "", (long long)sm.basis[i]);
+        printf("], \"costs\": [");
+        for (int64_t j = 0; j < sm.n; j++) {
+            if (j) printf(", ");
+            print_q(sm.costs[j]);
+        }
+        printf("], \"constant\": ");
+        print_q(sm.constant);
+        printf(", \"zcoef\": ");
+        print_q(sm.zcoef);
+        printf(", \"rows\": [");
+        for (int64_t i = 0; i < sm.m; i++) {
+            printf("%s[", i ? ", " : "");
+            for (int64_t j = 0; j <= sm.n; j++) {
+                if (j) printf(", ");
+                print_q(sm.rows[i * (sm.n + 1) + j]);
+            }
+            printf("]");
+        }
+        printf("], \"vars\": [");
+        for (int64_t v = 0; v < sm.nvars; v++)
+            printf("%s[\"%s\", %d, \"%s\", \"%s\"]", v ? ", " : "", sm.vars[v].name, sm.vars[v].relation,
+                   sm.vars[v].former, sm.vars[v].latter);
+        printf("]}\n");
+        lpf_free(&sm);
+        return 0;
+    }
+    lpf_solution sol;
+    if (lpf_solve(&sm, bigm, rule, device, &sol, err, sizeof err)) {
+        printf("{\"error\": \"%s\"}\n", err);
+        lpf_free(&sm);
+        return 1;
+    }
+    printf("{\"status\": \"%s\", \"pivots\": %lld", status_name(sol.status), (long long)sol.pivots);
+    if (sol.status == LPG_OPTIMAL) {
+        printf(", \"z\": %.17g, \"variables\": {", sol.z);
+        for (int64_t v = 0; v < sm.nvars; v++) printf("%s\"%s\": %.17g", v ? ", " : "", sm.vars[v].name, sol.vals[v]);
+        printf("}");
+    }
+    printf("}\n");
+    lpf_solution_free(&sol);
+    lpf_free(&sm);
+    return 0;
 }
 
 static int load_tableau_file(lpg_ctx **ctx, const char *path, int device) {
@@ -80,13 +164,19 @@ int main(int argc, char **argv) {
     long long m = 0, n = 0, pivots = (long long)1 << 40;
     unsigned long long seed = 20220518ull;
     int kind = LPG_GEN_DENSE, rule = LPG_RULE_DANTZIG, device = 0;
-    const char *file = NULL;
+    const char *file = NULL, *lpfile = NULL;
+    int dump = 0, bigm = 0;
     for (int a = 1; a < argc; a++) {
         if (!strcmp(argv[a], "--synthetic") && a + 2 < argc) {
             m = atoll(argv[++a]);
             n = atoll(argv[++a]);
         } else if (!strcmp(argv[a], "--tableau") && a + 1 < argc) {
             file = argv[++a];
+        } else if ((!strcmp(argv[a], "--lp") || !strcmp(argv[a], "--lp-dump")) && a + 1 < argc) {
+            dump = !strcmp(argv[a], "--lp-dump");
+            lpfile = argv[++a];
+        } else if (!strcmp(argv[a], "--big-m")) {
+            bigm = 1;
         } else if (!strcmp(argv[a], "--seed") && a + 1 < argc) {
             seed = strtoull(argv[++a], NULL, 10);
         } else if (!strcmp(argv[a], "--kind") && a + 1 < argc) {
@@ -101,6 +191,7 @@ int main(int argc, char **argv) {
             return usage(argv[0]);
         }
     }
+    if (lpfile) return run_lp(lpfile, dump, bigm, rule, device);
     lpg_ctx *ctx = NULL;
     int rc;
     if (file) {

@@ -171,6 +171,64 @@ def test_random_lps_match_the_reference_binary(tmp_path):
     assert compared >= 150, (compared, rejected, crashed)
 
 
+# ---- the C restatement (host/lpfront.c, behind host/lpgcli --lp) ----------------
+
+CLI = os.path.join(ROOT, "host", "lpgcli")
+SAN_CLI = os.path.join(ROOT, "integration", "_san", "lpgcli")
+needs_cli = pytest.mark.skipif(not os.path.exists(CLI), reason="host/lpgcli not built")
+
+
+def _c_dump(path, cli=CLI):
+    p = subprocess.run([cli, "--lp-dump", path], capture_output=True, text=True, timeout=30)
+    return p.returncode, json.loads(p.stdout)
+
+
+def _py_dump(text):
+    sm = F.build_smatrix(text)
+    return {"names": sm.display_names, "basis": sm.basis, "costs": [f"{c.numerator}/{c.denominator}" for c in sm.costs],
+            "constant": f"{sm.constant.numerator}/{sm.constant.denominator}",
+            "zcoef": f"{sm.zcoef.numerator}/{sm.zcoef.denominator}",
+            "rows": [[f"{x.numerator}/{x.denominator}" for x in r] for r in sm.rows],
+            "vars": [[it.name, it.relation, it.former, it.latter] for it in sm.vars.ordered()]}
+
+
+@needs_cli
+def test_c_front_end_equals_the_python_one(tmp_path):
+    """lpfront.c and frontend.py build the same SimplexMatrix and variable table
+    (or reject the same models) on every fixture and 200 random models; the
+    Python one is pinned to the reference binary above."""
+    files = [os.path.join(LP, f) for f in sorted(os.listdir(LP))]
+    rng = np.random.default_rng(99)
+    for t in range(200):
+        f = tmp_path / f"c{t}.txt"
+        f.write_text(_random_lp_rich(rng))
+        files.append(str(f))
+    for f in files:
+        text = open(f).read()
+        rc, got = _c_dump(f)
+        try:
+            exp = _py_dump(text)
+        except F.FrontendError as ex:
+            assert rc == 3 and "error" in got, (f, got, str(ex))
+            continue
+        assert rc == 0 and got == exp, (text, got, exp)
+
+
+@pytest.mark.skipif(not os.path.exists(SAN_CLI), reason="integration/_san/lpgcli not built")
+def test_c_front_end_under_asan_ubsan(tmp_path):
+    """The ASan + UBSan build of lpgcli on the fixtures and 40 random models, incl. rejected ones."""
+    files = [os.path.join(LP, f) for f in sorted(os.listdir(LP))]
+    rng = np.random.default_rng(7)
+    for t in range(40):
+        f = tmp_path / f"s{t}.txt"
+        f.write_text(_random_lp_rich(rng))
+        files.append(str(f))
+    for f in files:
+        p = subprocess.run([SAN_CLI, "--lp-dump", f], capture_output=True, text=True, timeout=60)
+        assert p.returncode in (0, 3) and "ERROR: AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr, \
+            (f, p.stderr[-2000:])
+
+
 # ---- device solve ------------------------------------------------------------
 
 @pytest.fixture(scope="module")
@@ -234,3 +292,18 @@ def test_device_solve_of_random_lps_matches_highs(lpg, tmp_path):
                 assert abs(sol.z - zref) < 1e-7 * max(1.0, abs(zref)), (text, method, sol.z, zref)
         solved += 1
     assert solved >= 40
+
+
+@needs_cli
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["", "--big-m"])
+def test_c_front_end_device_solve(lpg, method):
+    """host/lpgcli --lp: the reference's model files solved on the device from plain C."""
+    for name, z in KNOWN:
+        args = [CLI, "--lp", os.path.join(LP, name)] + ([method] if method else [])
+        p = subprocess.run(args, capture_output=True, text=True, timeout=120)
+        out = json.loads(p.stdout.strip().splitlines()[-1])
+        assert out["status"] == "OPTIMAL" and abs(out["z"] - z) < 1e-9 * max(1.0, abs(z)), (name, out)
+    p = subprocess.run([CLI, "--lp", os.path.join(LP, "a3_min_eq_neg.txt")], capture_output=True, text=True, timeout=120)
+    v = json.loads(p.stdout.strip().splitlines()[-1])["variables"]
+    assert abs(v["x1"] - 5 / 3) < 1e-12 and abs(v["x2"] - 7 / 3) < 1e-12 and v["x3"] == 0.0
