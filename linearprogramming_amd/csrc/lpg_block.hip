@@ -70,7 +70,10 @@ constexpr int kMaxWG = 256;         // records swept per phase: 4 per lane of on
 constexpr int kPer = kMaxWG / 64;
 constexpr int kRecPMax = 5;         // pricing record granules (k_pivot_block's NGP), space reserved per workgroup
 constexpr int kRecR = 2;            // ratio record:   {theta, key, tag} {piv, row, tag}
-constexpr int kMaxLds = 150 * 1024;   // dynamic LDS cap (the slices)
+#ifndef LPG_MAX_LDS_KB
+#define LPG_MAX_LDS_KB 150          // experiments: the dynamic LDS cap (the slices) in KB
+#endif
+constexpr int kMaxLds = LPG_MAX_LDS_KB * 1024;   // dynamic LDS cap (the slices)
 constexpr long long kSpinTicks = 200000000ll;   // s_memrealtime runs at 100 MHz: 2 s
 #ifndef LPG_SWEEP_SLEEP
 #define LPG_SWEEP_SLEEP 1           // s_sleep between record polls (64 clocks each)
@@ -631,7 +634,27 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         // k_prep_d's bookkeeping, stores only (a dependent load here would hold
         // back workgroup 0, and every sweep waits for the slowest workgroup):
         // the row's owner records the leaving variable it holds
-        if (wg == 0 && tid == 0) {
+#ifndef LPG_BOOK_LATE
+#define LPG_BOOK_LATE 0             // experiments: 1 = single-rank bookkeeping by wave 1 after the pricing record
+#endif
+        auto bookkeeping = [&]() {
+            st->slot[s].r = r;
+            D.rq[q] = rl;
+            st->npend = q + 1;
+            D.kq[q] = kt;
+            D.pv[q] = piv;
+            const int64_t np = np0 + t;
+            if (D.logk && np < logcap) {
+                D.logk[np] = kt;
+                D.logr[np] = r;
+            }
+            st->pivots = np + 1;
+            st->last_k = kt;
+            st->last_r = r;
+        };
+        if (!MR && LPG_BOOK_LATE) {
+            // below, after this workgroup's pricing record
+        } else if (wg == 0 && tid == 0) {
             st->slot[s].r = r;
             D.rq[q] = rl;
             if (MR) lvv = D.basis[r];                   // stored after the P exchange: its latency hides there
@@ -734,6 +757,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             rec_store(recP, (wg * NGP + 2) * 16, pack(0ull, 0u, tag));
             if (NOBJ == 2) rec_store(recP, (wg * NGP + 4) * 16, pack(0ull, 0u, tag));
         }
+        if (!MR && LPG_BOOK_LATE && wg == 0 && tid == 64) bookkeeping();   // nothing in the launch reads it
         LPG_BPUB(0, t);
         LPG_BPH(t, 3);
 
