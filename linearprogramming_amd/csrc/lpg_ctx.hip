@@ -142,7 +142,10 @@ static int fail(lpg_ctx *c, int code, const char *fmt, ...) {
 #define HIPCHK(c, x)                                                                         \
     do {                                                                                     \
         hipError_t e_ = (x);                                                                 \
-        if (e_ != hipSuccess) return fail((c), LPG_ERR_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+        if (e_ != hipSuccess) {                                                              \
+            (void)hipGetLastError(); /* a failed call (e.g. an OOM hipMalloc) must not fail the next launch check */ \
+            return fail((c), LPG_ERR_DEVICE, "%s: %s", #x, hipGetErrorString(e_));           \
+        }                                                                                    \
     } while (0)
 
 static Geo geo(const lpg_ctx *c) {
@@ -1404,7 +1407,6 @@ int lpg_solve_dual(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
     for (int64_t j = 1; j <= c->nact; j++)
         if (obj[j] < -c->eps_opt)
             return fail(c, LPG_ERR_STATE, "lpg_solve_dual: basis not dual feasible (d_%lld = %g)", (long long)j, obj[j]);
-    if ((rc = ensure_log(c, c->enq + max_pivots))) return rc;
     const Geo g = geo(c);
     const Launch L = lau(c);
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
@@ -1415,6 +1417,7 @@ int lpg_solve_dual(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
     lpg_result r;
     while (done < max_pivots) {
         const int64_t n = std::min(batch, max_pivots - done);
+        if ((rc = ensure_log(c, c->enq + n))) return rc;   // grown per batch (doubling), not to max_pivots up front
         for (int64_t q = 0; q < n; q++) {
             const int s = c->par;
             if (launch_dual_pivot(L, g, c->st, s, c->part, c->nsel, c->pp, c->pc, c->npp, c->skip, c->P, c->C[s]))

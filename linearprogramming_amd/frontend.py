@@ -392,8 +392,12 @@ def _invert_neg(terms: list, table: VarTable) -> None:
             t.inverted = True
 
 
-def standardize(m: Model) -> Model:
-    """LPStandardize (simplex.c:91-230), primal form (dual = 0)."""
+def standardize(m: Model, dual: bool = False) -> Model:
+    """LPStandardize (simplex.c:91-230). Primal form (dual = 0): rows with a
+    negative right-hand side are negated. Dual form (dual = 1, simplex.c:178-179):
+    every > / >= row is negated into < / <= instead, whatever the sign of b, so
+    each inequality gets a +1 slack (the dual simplex's starting basis; the
+    reference's router never reaches this branch, router.c:32-34)."""
     sub = [m.vars.max_x]
 
     def slack():
@@ -433,7 +437,7 @@ def standardize(m: Model) -> Model:
         i += 1
     for st in m.rows:
         b = st.right[0]
-        if _dec(b.coef) < 0:
+        if (not dual and _dec(b.coef) < 0) or (dual and st.relation > 0 and st.relation != 3):
             b.coef = -b.coef
             for t in st.left:
                 t.coef = -t.coef
@@ -508,9 +512,10 @@ def smatrix(m: Model) -> SMatrix:
                    [i for i, b in enumerate(basis) if b == 0], constant, m.zcoef, m.vars)
 
 
-def build_smatrix(text: str) -> SMatrix:
-    """LP text -> the reference's SimplexMatrix (Parser, LPTrans, LPStandardize, LPAlign, CreateSMatrix)."""
-    return smatrix(align(standardize(lp_trans(parse(text)))))
+def build_smatrix(text: str, dual: bool = False) -> SMatrix:
+    """LP text -> the reference's SimplexMatrix (Parser, LPTrans, LPStandardize, LPAlign, CreateSMatrix);
+    ``dual``: LPStandardize's dual form (for ``solve(method="dual")``)."""
+    return smatrix(align(standardize(lp_trans(parse(text)), dual=dual)))
 
 
 @dataclass
@@ -526,8 +531,10 @@ class LPSolution:
 def solve(sm: SMatrix, method: str = "two_phase", rule=None, device: int = 0) -> LPSolution:
     """The bridge's device solve (integration/lpg_bridge.c LPGSolveSMatrix) on liblpg:
     rows without a true unit basic column get artificials (two-phase by default,
-    ``method="big_m"`` for Big-M); the readout un-substitutes x <= 0 and free
-    variables as the reference's variable table records them."""
+    ``method="big_m"`` for Big-M; ``method="dual"``: the dual simplex from the
+    slack basis of a dual-form SimplexMatrix, which must be complete and dual
+    feasible); the readout un-substitutes x <= 0 and free variables as the
+    reference's variable table records them."""
     from . import _lib as L
     from .engine import Engine
     if rule is None:
@@ -539,6 +546,11 @@ def solve(sm: SMatrix, method: str = "two_phase", rule=None, device: int = 0) ->
         if j and any(sm.rows[q][j] != (1 if q == i else 0) for q in range(m)):
             basis[i] = 0
     nlack = sum(1 for b in basis if b == 0)
+    if method == "dual":
+        if nlack:
+            raise FrontendError("dual simplex: rows without a slack basis (equality rows); use build_smatrix(text, dual=True)")
+        if any(_dec(c) > 0 for c in sm.costs):
+            raise FrontendError("dual simplex: the slack basis is not dual feasible (a positive max-form cost)")
     nc = nc0 + nlack
     rows = np.zeros((m, nc), dtype=np.float64)
     for i, r in enumerate(sm.rows):
@@ -555,7 +567,11 @@ def solve(sm: SMatrix, method: str = "two_phase", rule=None, device: int = 0) ->
     with Engine(m, nc, device=device, flags=L.FLAG_BIG_M if bigm else 0) as e:
         e.load_rows(0, rows)
         e.set_basis(np.asarray(basis, dtype=np.int64))
-        if nlack == 0:
+        if method == "dual":
+            e.set_objective(cost)
+            r = e.solve_dual()
+            used = "dual"
+        elif nlack == 0:
             e.set_objective(cost)
             r = e.solve(rule=rule)
             used = "primal"
@@ -588,7 +604,7 @@ def solve(sm: SMatrix, method: str = "two_phase", rule=None, device: int = 0) ->
 
 def solve_text(text: str, method: str = "two_phase", rule=None, device: int = 0) -> LPSolution:
     """LP text (the reference's input format) -> the optimum on the device."""
-    return solve(build_smatrix(text), method=method, rule=rule, device=device)
+    return solve(build_smatrix(text, dual=method == "dual"), method=method, rule=rule, device=device)
 
 
 def main(argv=None) -> int:
@@ -599,15 +615,16 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=main.__doc__)
     ap.add_argument("path")
     ap.add_argument("--big-m", action="store_true", help="artificials by Big-M instead of two-phase")
+    ap.add_argument("--dual", action="store_true", help="dual form and the dual simplex (dual-feasible models)")
     ap.add_argument("--bland", action="store_true", help="Bland's rule instead of Dantzig's")
     a = ap.parse_args(argv)
+    method = "dual" if a.dual else ("big_m" if a.big_m else "two_phase")
     try:
-        sm = build_smatrix(open(a.path, "rb").read())
+        sm = build_smatrix(open(a.path, "rb").read(), dual=a.dual)
+        sol = solve(sm, method=method, rule=L.RULE_BLAND if a.bland else L.RULE_DANTZIG)
     except FrontendError as ex:
         print(ex)
         return 2
-    sol = solve(sm, method="big_m" if a.big_m else "two_phase",
-                rule=L.RULE_BLAND if a.bland else L.RULE_DANTZIG)
     print(f"{sol.status} after {sol.pivots} pivots ({sol.method})")
     if sol.status == "OPTIMAL":
         print(f"\tz = {sol.z:.12g}")

@@ -171,6 +171,34 @@ def test_random_lps_match_the_reference_binary(tmp_path):
     assert compared >= 150, (compared, rejected, crashed)
 
 
+DUAL_LP = "OF {\n\tmin:z=2x1+3x2\n}\nST {\n\tx1+x2>=4;\n\tx1+3x2>=6;\n\tx1>=0;\n\tx2>=0\n}\n"
+
+
+def test_dual_form():
+    """LPStandardize's dual branch (simplex.c:178-179): >= rows negated into <= with a
+    +1 slack each, b negative allowed, the slacks a complete basis. (The reference's
+    router never reaches it, router.c:32-34: parity unpinned, structure checked.)"""
+    sm = F.build_smatrix(DUAL_LP, dual=True)
+    assert sm.names == ["x1", "x2", "x3", "x4"] and sm.basis == [3, 4] and sm.lacking == []
+    assert sm.rows == [[-4, -1, -1, 1, 0], [-6, -1, -3, 0, 1]]
+    assert sm.costs == [-2, -3, 0, 0] and sm.zcoef == -1
+    primal = F.build_smatrix(DUAL_LP)
+    assert primal.lacking == [0, 1]                     # the primal form needs artificials instead
+    with pytest.raises(F.FrontendError, match="dual feasible"):
+        F.solve(F.build_smatrix("OF {\n max:z=x1\n}\nST {\n x1<=3;\n x1>=0\n}\n", dual=True), method="dual")
+
+
+def _random_dual_lp(rng):
+    n, m = int(rng.integers(1, 6)), int(rng.integers(1, 6))
+    rows = []
+    for _ in range(m):
+        terms = "+".join(f"{_rand_coef(rng, int(rng.integers(1, 9)))}x{j}" for j in range(1, n + 1))
+        rows.append(f"{terms}{rng.choice(['>=', '<='], p=[0.7, 0.3])}{int(rng.integers(1, 30))}")
+    rows += [f"x{j}>=0" for j in range(1, n + 1)]
+    obj = "+".join(f"{_rand_coef(rng, int(rng.integers(1, 9)))}x{j}" for j in range(1, n + 1))
+    return "OF {\n\tmin:z=" + obj + "\n}\nST {\n\t" + ";\n\t".join(rows) + "\n}\n"
+
+
 # ---- the C restatement (host/lpfront.c, behind host/lpgcli --lp) ----------------
 
 CLI = os.path.join(ROOT, "host", "lpgcli")
@@ -307,3 +335,20 @@ def test_c_front_end_device_solve(lpg, method):
     p = subprocess.run([CLI, "--lp", os.path.join(LP, "a3_min_eq_neg.txt")], capture_output=True, text=True, timeout=120)
     v = json.loads(p.stdout.strip().splitlines()[-1])["variables"]
     assert abs(v["x1"] - 5 / 3) < 1e-12 and abs(v["x2"] - 7 / 3) < 1e-12 and v["x3"] == 0.0
+
+
+@pytest.mark.gpu
+def test_dual_simplex_from_the_front_end(lpg):
+    """The dual form solved by the device's dual simplex equals the primal
+    (two-phase) optimum: the fixture-style model and 30 random dual-feasible ones."""
+    sol = F.solve_text(DUAL_LP, method="dual")
+    assert sol.status == "OPTIMAL" and sol.method == "dual" and abs(sol.z - 9.0) < 1e-12
+    assert abs(sol.variables["x1"] - 3.0) < 1e-12 and abs(sol.variables["x2"] - 1.0) < 1e-12
+    rng = np.random.default_rng(5)
+    for _ in range(30):
+        text = _random_dual_lp(rng)
+        d = F.solve_text(text, method="dual")
+        p = F.solve_text(text, method="two_phase")
+        assert d.status == p.status, (text, d, p)
+        if p.status == "OPTIMAL":
+            assert abs(d.z - p.z) < 1e-9 * max(1.0, abs(p.z)), (text, d.z, p.z)
