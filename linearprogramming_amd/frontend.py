@@ -62,7 +62,7 @@ def _strtol(s: str):
     if j < n and s[j] in "+-":
         j += 1
     k = j
-    while k < n and s[k].isdigit():
+    while k < n and s[k] in "0123456789":
         k += 1
     if k == j:
         return 0, n == 0
@@ -221,7 +221,7 @@ def _formula(s: str) -> Formula:
             else:
                 f.relation, side = 3, 1
         else:
-            if not cfc and not ch.isdigit() and ch not in "./":
+            if not cfc and ch not in "0123456789./":
                 coef = fractionize(buf) if buf else Fraction(1)
                 buf, cfc = "", True
             buf += ch
