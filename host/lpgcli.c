@@ -62,6 +62,26 @@ static char *read_all(const char *path) {
     return b;
 }
 
+/* a JSON string literal: quotes, backslashes and control characters escaped
+ * (error messages and variable names carry text from the model file) */
+static void json_str(const char *t) {
+    putchar('"');
+    for (const unsigned char *c = (const unsigned char *)t; *c; c++) {
+        if (*c == '"' || *c == '\\') printf("\\%c", *c);
+        else if (*c == '\n') printf("\\n");
+        else if (*c == '\t') printf("\\t");
+        else if (*c < 0x20) printf("\\u%04x", *c);
+        else putchar(*c);
+    }
+    putchar('"');
+}
+
+static void print_error(const char *err) {
+    printf("{\"error\": ");
+    json_str(err);
+    printf("}\n");
+}
+
 static void print_q(lpf_q q) { printf("\"%lld/%lld\"", (long long)q.num, (long long)q.den); }
 
 /* the reference model file -> SimplexMatrix (dump) or the device optimum */
@@ -73,12 +93,17 @@ static int run_lp(const char *path, int dump, int bigm, int rule, int device) {
     const int rc = lpf_build(text, &sm, err, sizeof err);
     free(text);
     if (rc) {
-        printf("{\"error\": \"%s\"}\n", err);
+        print_error(err);
         return 3;
     }
     if (dump) {
         printf("{\"names\": [");
-        for (int64_t j = 0; j < sm.n; j++) printf("%s\"%s%s\"", j ? ", " : "", sm.names[j], sm.inverted[j] ? "'" : "");
+        for (int64_t j = 0; j < sm.n; j++) {
+            char nm[256];
+            snprintf(nm, sizeof nm, "%s%s", sm.names[j], sm.inverted[j] ? "'" : "");
+            printf("%s", j ? ", " : "");
+            json_str(nm);
+        }
         printf("], \"basis\": [");
         for (int64_t i = 0; i < sm.m; i++) printf("%s%lld", i ? ", " : "", (long long)sm.basis[i]);
         printf("], \"costs\": [");
@@ -100,23 +125,33 @@ static int run_lp(const char *path, int dump, int bigm, int rule, int device) {
             printf("]");
         }
         printf("], \"vars\": [");
-        for (int64_t v = 0; v < sm.nvars; v++)
-            printf("%s[\"%s\", %d, \"%s\", \"%s\"]", v ? ", " : "", sm.vars[v].name, sm.vars[v].relation,
-                   sm.vars[v].former, sm.vars[v].latter);
+        for (int64_t v = 0; v < sm.nvars; v++) {
+            printf("%s[", v ? ", " : "");
+            json_str(sm.vars[v].name);
+            printf(", %d, ", sm.vars[v].relation);
+            json_str(sm.vars[v].former);
+            printf(", ");
+            json_str(sm.vars[v].latter);
+            printf("]");
+        }
         printf("]}\n");
         lpf_free(&sm);
         return 0;
     }
     lpf_solution sol;
     if (lpf_solve(&sm, bigm, rule, device, &sol, err, sizeof err)) {
-        printf("{\"error\": \"%s\"}\n", err);
+        print_error(err);
         lpf_free(&sm);
         return 1;
     }
     printf("{\"status\": \"%s\", \"pivots\": %lld", status_name(sol.status), (long long)sol.pivots);
     if (sol.status == LPG_OPTIMAL) {
         printf(", \"z\": %.17g, \"variables\": {", sol.z);
-        for (int64_t v = 0; v < sm.nvars; v++) printf("%s\"%s\": %.17g", v ? ", " : "", sm.vars[v].name, sol.vals[v]);
+        for (int64_t v = 0; v < sm.nvars; v++) {
+            printf("%s", v ? ", " : "");
+            json_str(sm.vars[v].name);
+            printf(": %.17g", sol.vals[v]);
+        }
         printf("}");
     }
     printf("}\n");

@@ -118,6 +118,10 @@ typedef struct {
     int32_t column_trade;       /* 1: the deferred path keeps the nonbasic columns contiguous (a column
                                    trade at every block's end; default from 2 GB per single rank, env
                                    LPG_NO_REORDER=0/1) */
+    int32_t residency_fallbacks;  /* persistent pivot launches that found their grid (every rank's) not resident
+                                     at once -- another kernel or process held CUs -- and handed the loop to the
+                                     two-kernel pair (pivot_wg is 0 from then on) */
+    int32_t pad0;
 } lpg_info_t;
 
 typedef struct {

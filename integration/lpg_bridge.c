@@ -220,11 +220,17 @@ short int LPGSolveSMatrix(SimplexMatrix *mx, double constant, double zcoef, shor
         printf("ERROR: device simplex failed: %s\n", lpg_last_error(ctx));
         goto out;
     }
-    if (has_m && res.status == LPG_OPTIMAL) {   /* an artificial left positive: infeasible (as lpg_solve_big_m) */
+    if (has_m && (res.status == LPG_OPTIMAL || res.status == LPG_UNBOUNDED)) {
+        /* an artificial left positive: infeasible, at an optimum and at a ray
+         * alike, with lpg_solve_big_m's tolerance (relative to sum |x_B|) */
+        double bsum = 0.0;
+        for (i = 0; i < (size_t) m; i++) bsum += fabs(xB[i]);
         for (i = 0; i < (size_t) m; i++)
-            if (basis[i] >= nc0 && xB[i] > 1e-9) res.status = LPG_INFEASIBLE;
-        if (lpg_get_rows(ctx, m, 1, rows, nc) != 0) goto out;   /* the M row: z = zM M + zR */
-        zM = rows[0];
+            if (basis[i] >= nc0 && xB[i] > 1e-9 * (bsum > 1.0 ? bsum : 1.0)) res.status = LPG_INFEASIBLE;
+        if (res.status == LPG_OPTIMAL) {
+            if (lpg_get_rows(ctx, m, 1, rows, nc) != 0) goto out;   /* the M row: z = zM M + zR */
+            zM = rows[0];
+        }
     }
     printf("\n---------------\n> Device Simplex (gfx950, lpg)%s\n\n",
            bigm ? ", Big-M (symbolic M)" : (nlack == 0 ? "" : ", two-phase"));

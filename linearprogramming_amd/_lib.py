@@ -41,7 +41,8 @@ class Info(ctypes.Structure):
                 ("row0", ctypes.c_int64), ("nrows", ctypes.c_int64),
                 ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("nobj", ctypes.c_int32), ("defer_k", ctypes.c_int32), ("pivot_wg", ctypes.c_int32),
-                ("bytes_per_pivot", ctypes.c_double), ("exchange", ctypes.c_int32), ("column_trade", ctypes.c_int32)]
+                ("bytes_per_pivot", ctypes.c_double), ("exchange", ctypes.c_int32), ("column_trade", ctypes.c_int32),
+                ("residency_fallbacks", ctypes.c_int32), ("pad0", ctypes.c_int32)]
 
 
 class Timing(ctypes.Structure):

@@ -55,6 +55,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "lpg_device.h"
 #include "lpg_internal.h"
@@ -273,6 +274,67 @@ __device__ bool xpoll_best(const Xch &X, uint32_t tag, uint64_t &h, uint32_t &l,
     return true;
 }
 
+// ---- residency census (the persistent launch needs every workgroup resident
+// at once; nothing guarantees it when another kernel or process holds CUs) --
+constexpr long long kResTicks = 100000ll;       // 1 ms for one rank's grid (normally resident within ~1 us)
+constexpr long long kResTicksMR = 2000000ll;    // 20 ms for every rank's (ranks drift apart by up to a block pass)
+constexpr uint64_t kGo = 1, kAbort = 2;
+
+// The first decision for launch `cl` wins: a word from an earlier launch is
+// replaced by (cl << 2) | d with a compare-and-swap; returns the decided word.
+template <typename W, int SCOPE>
+__device__ W decide(W *w, W cl, W d) {
+    W v = __hip_atomic_load(w, __ATOMIC_RELAXED, SCOPE);
+    while ((v >> 2) != cl)
+        if (__hip_atomic_compare_exchange_strong(w, &v, (cl << 2) | d, __ATOMIC_RELAXED, __ATOMIC_RELAXED, SCOPE))
+            return (cl << 2) | d;
+    return v;
+}
+
+// Thread 0 of every workgroup: count in, then wait for the decision. One
+// rank: the last of nwg arrivals decides GO (DevState::rcnt counts from
+// (cl - 1) * nwg: every earlier launch's workgroups all arrived, aborted or
+// not, before this one started); a workgroup that waits kResTicks decides
+// ABORT. Several ranks (X): each rank's last local arrival adds the rank to
+// rank 0's global count (tagged with this launch's exchange tag, the same on
+// every rank), the arrival that completes it decides GO in rank 0's global
+// decision word, and any workgroup of any rank that waits kResTicksMR
+// decides ABORT there: one word, so every rank takes the same decision.
+template <bool MR>
+__device__ bool census(DevState *st, int nwg, uint32_t cl, const Xch &X, uint32_t xtag) {
+    const uint32_t n =
+        __hip_atomic_fetch_add(&st->rcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - (cl - 1u) * (uint32_t)nwg + 1u;
+    uint64_t *gc = MR ? (uint64_t *)(X.base[0] + X.offG) : nullptr;   // {count tagged (xtag << 8)} ...
+    uint64_t *gd = MR ? gc + 8 : nullptr;                             // ... and the decision, a line apart
+    if (n == (uint32_t)nwg) {
+        if (!MR) {
+            decide<uint32_t, __HIP_MEMORY_SCOPE_AGENT>(&st->rdec, cl, (uint32_t)kGo);
+        } else {
+            uint64_t v = __hip_atomic_load(gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), nv;
+            for (;;) {
+                nv = (v >> 8) == (uint64_t)xtag ? v + 1 : (((uint64_t)xtag << 8) | 1u);
+                if (__hip_atomic_compare_exchange_strong(gc, &v, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_SYSTEM))
+                    break;
+            }
+            if ((int)(nv & 0xff) == X.world) decide<uint64_t, __HIP_MEMORY_SCOPE_SYSTEM>(gd, xtag, kGo);
+        }
+    }
+    const long long t0 = (long long)wall_clock64();
+    for (;;) {
+        uint64_t v;
+        if (MR) v = __hip_atomic_load(gd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else v = __hip_atomic_load(&st->rdec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v >> 2) == (MR ? (uint64_t)xtag : (uint64_t)cl)) return (v & 3) == kGo;
+        if ((long long)wall_clock64() - t0 > (MR ? kResTicksMR : kResTicks)) {
+            v = MR ? decide<uint64_t, __HIP_MEMORY_SCOPE_SYSTEM>(gd, xtag, kAbort)
+                   : decide<uint32_t, __HIP_MEMORY_SCOPE_AGENT>(&st->rdec, cl, (uint32_t)kAbort);
+            return (v & 3) == kGo;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
 }  // namespace
 
 #ifdef LPG_PHASES
@@ -373,6 +435,7 @@ struct BlockArgs {
     u4 *rec;                     // nwg * (kRecPMax + kRecR) granules
     uint32_t tag0;               // tag of pivot i of this launch = tag0 + 1 + i (never repeats per context)
     int nwg, cw, rw, ks;         // workgroups, columns / rows per slice, LDS slots
+    uint32_t cl;                 // residency census: this launch's index since the DevState was reset (1-based)
 };
 
 // MR (multi-rank, row partition; Xch attached): the leaving row is the
@@ -417,6 +480,21 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     const __amdgpu_buffer_rsrc_t recP = rsrc(a.rec, nwg * NGP * 16);
     const __amdgpu_buffer_rsrc_t recR = rsrc(a.rec + nwg * kRecPMax, nwg * kRecR * 16);
     DevState *st = a.st;
+
+    // ---- residency census: the whole grid (every rank's) resident, or nothing
+    {
+        __shared__ int go;
+        if (tid == 0) go = census<MR>(st, nwg, a.cl, a.X, a.xtag0);
+        __syncthreads();
+        if (!go) {
+            if (tid == 0) {               // every workgroup alike: no pivot ran; the loop stops until the host
+                st->slot[0].status = ITER_LIMIT;   // has switched to the pair (lpg_ctx.hip recover_residency)
+                st->slot[1].status = ITER_LIMIT;
+                st->stall = kStallResidency;
+            }
+            return;
+        }
+    }
 
     // ---- launch start: everything here was written before the launch
     int s = a.s0;
@@ -922,9 +1000,9 @@ int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, i
 
 int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, int s0, int q0, int n, Cand *part,
                        int ncand, const Cand *cin, int ncin, const double *Cs0, double *Cs1, const Defer &D,
-                       void *rec, uint32_t tag0, int nwg, int cw, int rw, int ks, size_t lds, const Xch *X,
-                       uint32_t xtag0) {
-    if (n < 1 || q0 < 0 || q0 + n > ks || ks > 64 || nwg < 1 || nwg > kMaxWG || ncand < nwg) return -1;
+                       void *rec, uint32_t tag0, int nwg, int cw, int rw, int ks, size_t lds, uint32_t cl,
+                       const Xch *X, uint32_t xtag0) {
+    if (n < 1 || q0 < 0 || q0 + n > ks || ks > 64 || nwg < 1 || nwg > kMaxWG || ncand < nwg || cl < 1) return -1;
     if (X && (X->world < 1 || X->world > 64 || X->nblk < nwg || X->nx < 1)) return -1;
     if ((int64_t)nwg * cw < ((g.ncols + 1) & ~(int64_t)1) || (int64_t)nwg * rw < g.nloc) return -1;
     if (g.nobj != 1 && g.nobj != 2) return -1;
@@ -950,15 +1028,21 @@ int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, in
     a.cw = cw;
     a.rw = rw;
     a.ks = ks;
+    a.cl = cl;
     hipStream_t stream = (hipStream_t)L.stream;
+    // the dynamic-LDS limit is a per-device attribute: set once per device
+    // (bit `dev` of a per-kernel mask; ranks as threads may race to set it,
+    // which is harmless)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
 #define LPG_PB(R, NO, M)                                                                                \
     do {                                                                                                \
-        static bool attr = false;                                                                       \
-        if (!attr) {                                                                                    \
+        static std::atomic<unsigned long long> attr{0};                                                 \
+        if (!((attr.load(std::memory_order_acquire) >> dev) & 1ull)) {                                   \
             if (hipFuncSetAttribute((const void *)k_pivot_block<R, NO, M>,                              \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds) != hipSuccess) \
                 return -1;                                                                              \
-            attr = true;                                                                                \
+            attr.fetch_or(1ull << dev, std::memory_order_acq_rel);                                      \
         }                                                                                               \
         hipLaunchKernelGGL((k_pivot_block<R, NO, M>), dim3(nwg), dim3(kNT), lds, stream, a);           \
     } while (0)

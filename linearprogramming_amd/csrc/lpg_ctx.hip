@@ -71,9 +71,12 @@ struct lpg_ctx {
     size_t pb_lds = 0;
     void *rec = nullptr;          // its records (zeroed once; tags never repeat within a context)
     uint32_t tag = 0;
+    uint32_t pb_launch = 0;       // persistent launches since the DevState was reset (the census index)
+    int64_t lost = 0;             // pivots enqueued on launches a residency census stopped (lpg_sync re-runs them)
+    int res_fallbacks = 0;        // residency censuses that failed (lpg_info: the pair took over)
     // owner-push exchange of the multi-rank deferred path (Xch, lpg_internal.h)
     char *xbuf = nullptr;         // this rank's exchange buffer
-    int64_t xbytes = 0, xoffF = 0, xoffC = 0;
+    int64_t xbytes = 0, xoffF = 0, xoffC = 0, xoffG = 0;
     int xnblk = 0, xnx = 0;
     bool xuncached = false;
     char **xbase = nullptr;       // device array of the world buffers
@@ -379,6 +382,13 @@ static int canonicalize(lpg_ctx *c) {
 // not) works with nsel_d, the generic kernels with nsel.
 static int cand_per_rank(const lpg_ctx *c) { return (c->defer_k > 0 && c->fast_pivot) ? c->nsel_d : c->nsel; }
 
+// Doubles of the pivot row the allreduce exchanges: the columns the prep
+// kernels write, [0, ncols) plus the even padding column k_flushw reads in
+// pairs -- never the rest of the ld pitch, which no kernel writes (round 2
+// summed that uninitialised padding across ranks: the overflow warning of
+// tests/test_gpu_dist.py's host transport).
+static int64_t prow_count(const lpg_ctx *c) { return (c->ncols + 1) & ~(int64_t)1; }
+
 static int exchange_candidates(lpg_ctx *c) {
     if (!has_comm(c)) return 0;
     return comm_allgather(c, c->part, c->cand, sizeof(Cand) * (size_t)cand_per_rank(c));
@@ -465,11 +475,13 @@ static int enqueue_blocks(lpg_ctx *c, int64_t npiv, int rule) {
             X.tag = c->xtag;
             X.offF = c->xoffF;
             X.offC = c->xoffC;
+            X.offG = c->xoffG;
         }
         if (launch_pivot_block(lau(c), g, rule, c->st, s0, c->pend, n, c->part, ncand, cin, ncin, c->C[s0], c->C[s1],
                                defer_of(c, c->pend), c->rec, c->tag, c->pb_nwg, c->pb_cw, c->pb_rw, c->defer_k,
-                               c->pb_lds, mr ? &X : nullptr, c->xtag))
+                               c->pb_lds, c->pb_launch + 1, mr ? &X : nullptr, c->xtag))
             return fail(c, LPG_ERR_DEVICE, "pivot block launch failed");
+        c->pb_launch++;
         if (mr) {
             c->xtag += (uint32_t)n;
             c->x_from_cand = false;
@@ -608,6 +620,7 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
             X.tag = c->xtag;
             X.offF = c->xoffF;
             X.offC = c->xoffC;
+            X.offG = c->xoffG;
             if (launch_prep_x(L, g, rule, c->st, s, c->cand, ncand_d, P, c->C[s], c->pp, c->npp_d, D, X))
                 return fail(c, LPG_ERR_DEVICE, "prep launch failed");
             if (launch_select_x(L, g, rule, c->st, s, s1, c->C[s], c->C[s1], c->pp, c->npp_d, c->basis, c->part,
@@ -624,7 +637,7 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
         if (D.on && c->fast_pivot) {            // deferred, with a communicator: the pair around the exchange
             if (launch_prep_dm(L, g, rule, c->st, s, c->cand, ncand_d, P, c->C[s], c->npp_d, D))
                 return fail(c, LPG_ERR_DEVICE, "prep launch failed");
-            if ((rc = comm_allreduce_sum(c, P, (size_t)c->ld))) return rc;
+            if ((rc = comm_allreduce_sum(c, P, (size_t)prow_count(c)))) return rc;
             if (launch_price(L, g, rule, 1, c->st, s, P, c->C[s], c->pp, c->pc, c->npp, true, c->colmap, c->inv))
                 return fail(c, LPG_ERR_DEVICE, "price launch failed");
             if (launch_select_dm(L, g, rule, c->st, s, s1, c->C[s], c->C[s1], c->pp, c->npp, c->basis, c->part,
@@ -640,7 +653,7 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
         if (launch_prep(L, g, rule, fuse, c->st, s, c->cand, ncand, P, c->C[s], c->pp, c->pc, c->npp, D))
             return fail(c, LPG_ERR_DEVICE, "prep launch failed");
         if (!fuse) {
-            if ((rc = comm_allreduce_sum(c, P, (size_t)c->ld))) return rc;
+            if ((rc = comm_allreduce_sum(c, P, (size_t)prow_count(c)))) return rc;
             if (launch_price(L, g, rule, 1, c->st, s, P, c->C[s], c->pp, c->pc, c->npp, D.on != 0))
                 return fail(c, LPG_ERR_DEVICE, "price launch failed");
         }
@@ -662,12 +675,41 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule) {
     return 0;
 }
 
+// A persistent launch found its grid (every rank's, on a communicator) not
+// resident at once -- another kernel or process held CUs -- and stopped
+// before its first pivot; every pivot launch after it did nothing (both
+// slots non-RUNNING), the flushes applied the pivots that had run. The loop
+// continues on the two-kernel pair, which needs no co-residency: the next
+// enqueue bootstraps (flush, then price and ratio test from the current
+// tableau, i.e. the choices the persistent launch would have made), so the
+// pivot sequence is unchanged. Every rank sees the same census decision
+// (rank 0's word, lpg_block.hip), so on a communicator every rank recovers
+// at the same launch and the bootstrap's collectives match.
+static int recover_residency(lpg_ctx *c, const DevState &h) {
+    c->persist = false;
+    c->persist_x = false;
+    c->pmr = false;
+    if (!has_comm(c)) c->nsel_d = pivot_d_blocks(geo(c), 1, c->pivot_nt);   // <= the allocation (max(nsel_d, nwg))
+    c->lost += std::max<int64_t>(c->enq - h.pivots, 0);
+    c->enq = h.pivots;
+    c->pend = (int)h.npend;
+    c->booted = false;
+    c->res_fallbacks++;
+    HIPCHK(c, hipMemsetAsync(&c->st->stall, 0, sizeof(int64_t), c->stream));
+    return 0;
+}
+
 static int read_result(lpg_ctx *c, lpg_result *out, int rule) {
     DevState h;
     HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));
     double z = 0;
     HIPCHK(c, hipMemcpyAsync(&z, c->T + (c->nloc + c->nobj - 1) * c->ld, sizeof z, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (h.stall == kStallResidency) {
+        int rc = recover_residency(c, h);
+        if (rc) return rc;
+        h.stall = 0;
+    }
     if (h.stall == 2 || h.stall == 3)
         return fail(c, LPG_ERR_COMM, "owner-push exchange: rank %d waited > 2 s for the %s (a rank stopped, or the "
                     "buffers are not shared; LPG_EXCHANGE=rccl keeps the collectives)", c->rank,
@@ -702,6 +744,8 @@ static int reset_state(lpg_ctx *c) {
     c->enq = 0;
     c->pend = 0;
     c->touched_mark = 0;
+    c->pb_launch = 0;      // the census counts from 0 again (DevState::rcnt / rdec are zero)
+    c->lost = 0;
     return 0;
 }
 
@@ -890,6 +934,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         hipMemset(c->P, 0, (size_t)c->ld * sizeof(double)) != hipSuccess ||
         hipMemset(c->basis, 0, (size_t)m * sizeof(int64_t)) != hipSuccess ||
         (c->Cbuf && hipMemset(c->Cbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->cs * sizeof(double)) != hipSuccess) ||
+        (c->Pbuf && hipMemset(c->Pbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->ld * sizeof(double)) != hipSuccess) ||
         (c->zrow && hipMemset(c->zrow, 0, (size_t)c->ld * sizeof(double)) != hipSuccess) ||
         (c->rec && hipMemset(c->rec, 0, (size_t)block_records_bytes(c->pb_nwg)) != hipSuccess) ||
         (c->colmap && (launch_iota(lau(c), c->colmap, c->ld) || launch_iota(lau(c), c->inv, c->ld)))) {
@@ -971,7 +1016,7 @@ static int ensure_xbuf(lpg_ctx *c) {
     if (!(c->defer_k > 0 && c->fast_pivot)) return fail(c, LPG_ERR_STATE, "push exchange needs the deferred pivot pair");
     c->xnblk = std::max(c->npp_d, c->pmr ? c->pb_nwg : 0);   // P chunk flags: prep blocks / k_pivot_block slices
     c->xnx = c->nsel_d;
-    c->xbytes = xch_bytes(c->ld, c->world, c->xnblk, c->xnx, &c->xoffF, &c->xoffC);
+    c->xbytes = xch_bytes(c->ld, c->world, c->xnblk, c->xnx, &c->xoffF, &c->xoffC, &c->xoffG);
     // uncached: a peer's stores over xGMI land in this GPU's HBM behind its
     // L2; with L2 out of the path the system-scope loads cannot hit a stale line
     void *p = nullptr;
@@ -1088,6 +1133,8 @@ int lpg_info(const lpg_ctx *c, lpg_info_t *o) {
     o->bytes_per_pivot = 16.0 * (double)(c->nloc + c->nobj) * (double)c->ncols;
     o->exchange = c->xmode ? (c->xuncached ? 2 : 1) : 0;
     o->column_trade = reorders(c) ? 1 : 0;
+    o->residency_fallbacks = c->res_fallbacks;
+    o->pad0 = 0;
     return 0;
 }
 
@@ -1244,7 +1291,19 @@ int lpg_sync(lpg_ctx *c, lpg_result *out) {
     if (!c) return fail(c, LPG_ERR_ARG, "ctx is NULL");
     int rc;
     if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
-    return read_result(c, out, c->boot_rule);
+    lpg_result r;
+    if ((rc = read_result(c, &r, c->boot_rule))) return rc;
+    // pivots a residency census dropped run now, on the pair (at most once:
+    // the persistent form is off after a recovery)
+    if (c->lost > 0 && r.status == LPG_ITER_LIMIT) {
+        const int64_t n = c->lost;
+        c->lost = 0;
+        if ((rc = lpg_enqueue(c, n, c->boot_rule)) || (rc = materialize(c)) || (rc = read_result(c, &r, c->boot_rule)))
+            return rc;
+    }
+    c->lost = 0;
+    if (out) *out = r;
+    return 0;
 }
 
 int lpg_solve(lpg_ctx *c, int64_t max_pivots, int rule, lpg_result *out) {
@@ -1260,19 +1319,24 @@ int lpg_solve(lpg_ctx *c, int64_t max_pivots, int rule, lpg_result *out) {
             return 0;
         }
     }
-    int64_t done = 0, batch = 8;
+    // max_pivots counts pivots the device applies: a launch a residency census
+    // stopped (recover_residency) applied none, and its pivots are re-run
+    int64_t have = device_pivots(c), batch = 8;
+    if (have < 0) return fail(c, LPG_ERR_DEVICE, "reading pivot count failed");
+    const int64_t target = max_pivots > INT64_MAX - have ? INT64_MAX : have + max_pivots;
     if (max_pivots == 0) {
         if (!c->booted || c->boot_rule != rule)
             if ((rc = enqueue(c, 0, rule))) return rc;
     }
-    while (done < max_pivots) {
-        const int64_t n = std::min(batch, max_pivots - done);
+    while (have < target) {
+        const int64_t n = std::min(batch, target - have);
         if ((rc = lpg_enqueue(c, n, rule))) return rc;
-        done += n;
         if ((rc = read_result(c, &r, rule))) return rc;
         if (r.status != LPG_ITER_LIMIT) break;
+        have = r.pivots;
         batch = std::min<int64_t>(batch * 2, 256);
     }
+    c->lost = 0;
     if ((rc = materialize(c))) return rc;
     return read_result(c, out, rule);
 }

@@ -51,9 +51,13 @@ struct DevState {
     unsigned long long work[2];   // k_update work-item dequeue heads, per pivot parity (reset by k_prep)
     int64_t npend;                // deferred pivots applied but not yet flushed (prep_t sets q + 1)
     unsigned long long fwork;     // k_flush work-item dequeue head (reset with npend after each flush)
-    int64_t stall;                // set by k_pivot_block when a workgroup gave up waiting (lpg_block.hip)
+    int64_t stall;                // set by k_pivot_block when a workgroup gave up waiting (lpg_block.hip);
+                                  // kStallResidency: a launch found its grid not co-resident and did nothing
     int64_t stall_info[4];        // its view then: phase (1 P, 2 S), expected tag, record index, tag seen
+    uint32_t rcnt;                // k_pivot_block residency census: arrivals (launch L's count from L * nwg)
+    uint32_t rdec;                // its decision word: (L << 2) | kGo / kAbort (single rank)
 };
+constexpr int64_t kStallResidency = 4;
 
 // Pending-pivot buffers of the deferred update (Defer::on == 0: eager mode).
 struct Defer {
@@ -89,6 +93,7 @@ struct Xch {
     int from_cand;                // 1: this pivot's candidates are in `cand` (after a bootstrap), not in xC
     uint32_t tag;                 // this pivot's tag (its candidates, its P flags); select publishes tag + 1
     int64_t offF, offC;           // byte offsets of xF and xC (xP at 0)
+    int64_t offG;                 // byte offset of the residency census words {gcnt, gdec} (rank 0's are used)
 };
 
 // Ratio-test candidate: lexicographic (theta, key); row < 0 = none.
@@ -164,7 +169,7 @@ int launch_prep_x(const Launch &L, const Geo &g, int rule, DevState *st, int s, 
 int launch_select_x(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, const double *Cs,
                     double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part, int nsel,
                     const Defer &D, const Xch &X);
-int64_t xch_bytes(int64_t ld, int world, int nblk, int nx, int64_t *offF, int64_t *offC);
+int64_t xch_bytes(int64_t ld, int world, int nblk, int nx, int64_t *offF, int64_t *offC, int64_t *offG);
 int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, const double *Cs,
                      double *Cs1, const PricePart *pp, int npp, const int64_t *basis, Cand *part, int nsel,
                      const Defer &D);
@@ -179,10 +184,15 @@ int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, i
 // cin / ncin: the first pivot's ratio candidates (part itself on one rank).
 // X != nullptr: multi-rank over the owner-push exchange (the same nwg / cw / rw
 // on every rank), exchange tags xtag0, xtag0 + 1, ...
+// Residency: every launch first counts its workgroups in (census launch
+// index `cl`, DevState::rcnt / rdec; with X, every rank's through rank 0's
+// exchange words): if the whole grid is not resident within a bound, the
+// launch does nothing, stops the loop (both slots non-RUNNING) and sets
+// DevState::stall = kStallResidency; the host then continues on the pair.
 int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, int s0, int q0, int n, Cand *part,
                        int ncand, const Cand *cin, int ncin, const double *Cs0, double *Cs1, const Defer &D,
-                       void *rec, uint32_t tag0, int nwg, int cw, int rw, int ks, size_t lds, const Xch *X = nullptr,
-                       uint32_t xtag0 = 0);
+                       void *rec, uint32_t tag0, int nwg, int cw, int rw, int ks, size_t lds, uint32_t cl,
+                       const Xch *X = nullptr, uint32_t xtag0 = 0);
 // Apply the pending pivots (st->npend <= kmax) to constraint rows 0..nloc-1.
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which);
 // ... in two parts: the block pass itself (k_flushw / k_flushm / k_flush), then

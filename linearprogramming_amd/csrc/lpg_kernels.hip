@@ -304,7 +304,9 @@ __global__ __launch_bounds__(kBlock) void k_prep(double *__restrict__ T, Geo g, 
     PricePart pbest{0.0, -1, 0, 0};
     bool live = false;
     if (j2 < nvec) {
-        d2 p = d2{0.0, 0.0};
+        // a rank that does not hold row r contributes -0, the identity of the
+        // allreduce that follows (+0 would turn an owner's -0 into +0)
+        d2 p = (FUSE || own) ? d2{0.0, 0.0} : d2{-0.0, -0.0};
         if (own) {
             if (DEFER) {   // row r of the current tableau: the pending chain
                 // chunks of 16 pending rows: all loads of a chunk in flight at once
@@ -1182,12 +1184,14 @@ int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int 
 }
 
 // Owner-push exchange: the buffer's size and the offsets of its parts (256-byte aligned).
-int64_t xch_bytes(int64_t ld, int world, int nblk, int nx, int64_t *offF, int64_t *offC) {
+int64_t xch_bytes(int64_t ld, int world, int nblk, int nx, int64_t *offF, int64_t *offC, int64_t *offG) {
     const int64_t f = (2 * (int64_t)world * ld * (int64_t)sizeof(double) + 255) & ~(int64_t)255;   // xP[2][world][ld]
     const int64_t c = (f + 2 * (int64_t)world * nblk * 4 + 255) & ~(int64_t)255;                  // xF[2][world][nblk]
+    const int64_t gg = (c + 2 * (int64_t)world * nx * 6 * 8 + 255) & ~(int64_t)255;               // xC[2][world][nx][6]
     if (offF) *offF = f;
     if (offC) *offC = c;
-    return c + 2 * (int64_t)world * nx * 6 * 8;
+    if (offG) *offG = gg;
+    return gg + 256;                                                                               // {gcnt, gdec}
 }
 
 int launch_prep_x(const Launch &L, const Geo &g, int rule, DevState *st, int s, const Cand *cand, int ncand,

@@ -242,6 +242,18 @@ def test_c_front_end_equals_the_python_one(tmp_path):
         assert rc == 0 and got == exp, (text, got, exp)
 
 
+@needs_cli
+@pytest.mark.parametrize("bad", ['max:z=3x1+5"x2', 'max:z=3x1+5\\x2', 'max:z=3x1+5\x01x2'])
+def test_c_front_end_error_is_valid_json(tmp_path, bad):
+    """Error text quotes the model's own bytes ("Invalid variable name: ..."):
+    quotes, backslashes and control characters are escaped, so the line stays
+    one valid JSON object."""
+    f = tmp_path / "bad.txt"
+    f.write_bytes(("OF {\n\t" + bad + "\n}\nST {\n\tx1<=4;\n\tx1>=0\n}\n").encode())
+    rc, got = _c_dump(str(f))
+    assert rc == 3 and got["error"].startswith("ERROR:")
+
+
 @pytest.mark.skipif(not os.path.exists(SAN_CLI), reason="integration/_san/lpgcli not built")
 def test_c_front_end_under_asan_ubsan(tmp_path):
     """The ASan + UBSan build of lpgcli on the fixtures and 40 random models, incl. rejected ones."""

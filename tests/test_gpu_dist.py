@@ -44,9 +44,23 @@ class ThreadComm:
     def allreduce(self, rank, arr: np.ndarray) -> np.ndarray:
         self.slots[rank] = arr
         self.bar.wait()
+        # The engine's allreduces are broadcasts in disguise: the
+        # pivot row from its owner, every other rank sending exactly -0, and the
+        # objective chain from the rank whose turn it is, the others +0. So at
+        # most one rank contributes anything but zeros, every other rank's
+        # buffer is one signed zero throughout, and the sum is the contributor's
+        # buffer bit for bit (round 2 summed uninitialised padding here).
+        bits = [np.ascontiguousarray(s).view(np.uint64) for s in self.slots]
+        live = [q for q in range(self.world) if np.any(bits[q] << np.uint64(1))]
+        assert len(live) <= 1, f"ranks {live} both contributed to one exchange"
+        for q in range(self.world):
+            if q not in live:
+                assert np.all(bits[q] == bits[q][0]), f"rank {q} sent a mix of +0 and -0"
         acc = self.slots[0].copy()
         for q in range(1, self.world):
             acc = acc + self.slots[q]
+        if live and all(bits[q][0] == np.uint64(1 << 63) for q in range(self.world) if q != live[0]):
+            assert np.array_equal(acc.view(np.uint64), bits[live[0]]), "the sum is not the owner's row"
         self.bar.wait()
         return acc
 

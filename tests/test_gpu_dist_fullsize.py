@@ -1,0 +1,166 @@
+"""The row partition at BASELINE.json's full sizes, two processes on the one GPU.
+
+BASELINE config 4 is "row-partitioned across 8 x MI355X": the multi-rank path
+(lpg_create_dist + a communicator + the owner-push exchange) is
+what the driver's 8-GPU run takes first. Here two ranks, one process each,
+share the lease's GPU through IPC-mapped exchange buffers (the layout of one
+process per GPU), at the full sizes:
+
+* config 3 (16384 x 32768, 8192 rows per rank), 200 pivots = three whole
+  64-pivot blocks (each ending in the column trade, the block pass and the
+  pivot-row rewrite on every rank) and a partial block flushed by the readout;
+  bitwise against the C oracle: pivot log, basis, objective row, every pivot
+  row and 64 sampled rows per rank.
+  - with the two-kernel pair (LPG_PERSIST_MR=0);
+  - with the persistent multi-rank launch left on: two 198-workgroup grids do
+    not fit one GPU's 256 CUs at once, so the launch's residency census
+    (lpg_block.hip) stops it before its first pivot on BOTH ranks (one
+    decision word) and the library continues on the pair by itself --
+    lpg_info.residency_fallbacks counts it -- instead of waiting 2 s and
+    failing (round 2).
+* config 4's shape (65536 x 131072, 32768 rows and 51.5 GB per rank, blocks
+  of 128 pivots, the multi-rank column trade over 196,609 columns), 320
+  pivots: bitwise equal to the single-rank engine (partition invariance: log,
+  basis, objective row, column 0, every pivot row and 64 sampled rows per
+  rank), plus unit basic columns on those rows and b >= 0 on every row.
+
+Reference: the loop simplex.c:40 -> :65 lacks.
+"""
+from __future__ import annotations
+
+import os
+import pickle
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+from oracle.lpo import Oracle
+
+pytestmark = pytest.mark.gpu
+SEED = 20220518
+
+
+@pytest.fixture(scope="module")
+def lpg():
+    import linearprogramming_amd as lpg
+    lpg.load()
+    assert lpg.device_count() >= 1, "no GPU visible"
+    return lpg
+
+
+def _sample(m, world, rank, k, seed):
+    """k sampled global rows of rank `rank`'s block (floor(m p / W) split)."""
+    r0, r1 = m * rank // world, m * (rank + 1) // world
+    rng = np.random.default_rng(seed + rank)
+    return sorted(set(rng.choice(np.arange(r0, r1), k, replace=False).tolist()) | {r0, r1 - 1})
+
+
+def _worker(rank, world, port, m, n, seed, pivots, outdir, env):
+    os.environ.update(env)
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import linearprogramming_amd as lpg
+
+    def allgather(b: bytes) -> bytes:
+        t = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        return b"".join(bytes(o.numpy()) for o in outs)
+
+    def allreduce(a: np.ndarray) -> np.ndarray:
+        t = torch.from_numpy(a)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.numpy()
+
+    e = lpg.Engine(m, n + m + 1, world=world, rank=rank)
+    e.comm_init_host(allgather, allreduce)
+    h = allgather(e.push_handle())
+    e.comm_init_push([h[64 * r:64 * r + 64] for r in range(world)])
+    wg0 = e.info.pivot_wg
+    e.generate(n, seed, lpg.GEN_DENSE)
+    e.reserve_log(pivots + 8)
+    res = e.solve(pivots, lpg.RULE_DANTZIG)
+    info = e.info
+    k, r = e.get_log()
+    basis = e.get_basis()
+    rows = sorted(set(_sample(m, world, rank, 64, seed)) | {int(x) for x in r if info.row0 <= x < info.row0 + info.nrows})
+    out = dict(status=res.status, pivots=res.pivots, objective=res.objective, log=(k, r), basis=basis,
+               obj=e.get_rows(m, 1)[0], rows={i: e.get_rows(i, 1)[0] for i in rows}, x0=e.get_column0(),
+               wg0=wg0, wg=info.pivot_wg, fallbacks=info.residency_fallbacks, exchange=info.exchange,
+               defer=info.defer_k, row0=info.row0, nrows=info.nrows)
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(out, f)
+    e.close()
+    dist.destroy_process_group()
+
+
+def _run(world, m, n, pivots, env):
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, port, m, n, SEED, pivots, d, env), nprocs=world, join=True)
+        return [pickle.load(open(os.path.join(d, f"r{q}.pkl"), "rb")) for q in range(world)]
+
+
+def _check_against(parts, m, pivots, log, basis, obj, row_of):
+    """Every rank equals the reference run (the oracle or the single-rank engine)."""
+    for p in parts:
+        assert p["pivots"] == pivots and p["status"] == 4              # ITER_LIMIT: the budget ran out first
+        assert np.array_equal(p["log"][0], log[0]) and np.array_equal(p["log"][1], log[1])
+        assert np.array_equal(p["basis"], basis)
+        assert np.array_equal(p["obj"], obj), "objective row"
+        pivot_rows = {int(x) for x in log[1]}
+        own = {i for i in pivot_rows if p["row0"] <= i < p["row0"] + p["nrows"]}
+        assert own <= set(p["rows"]), "a pivot row was not read back"
+        for i, ri in p["rows"].items():
+            assert np.array_equal(ri, row_of(i)), f"rank row {i}"
+            assert ri[basis[i]] == 1.0 and np.count_nonzero(ri[basis]) == 1, f"row {i}: basic columns not unit"
+        assert np.all(p["x0"] >= 0.0)
+    assert sum(p["nrows"] for p in parts) == m
+
+
+@pytest.mark.parametrize("mr", ["0", None])
+def test_config3_two_processes_bitwise(lpg, mr):
+    m, n, piv = 16384, 32768, 200
+    env = {"LPG_PERSIST_MR": mr} if mr is not None else {}
+    parts = _run(2, m, n, piv, env)
+    assert all(p["defer"] == 64 and p["exchange"] in (1, 2) for p in parts)
+    if mr == "0":
+        assert all(p["wg0"] == 0 and p["wg"] == 0 and p["fallbacks"] == 0 for p in parts)
+    else:
+        # the persistent form was on; two such grids cannot be resident on one GPU:
+        # the census stopped the first launch on both ranks and the pair took over
+        assert all(p["wg0"] > 0 for p in parts), "the persistent multi-rank form was not selected"
+        assert all(p["fallbacks"] >= 1 and p["wg"] == 0 for p in parts), [(p["fallbacks"], p["wg"]) for p in parts]
+    o = Oracle(m, n + m + 1, nthreads=min(16, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    o.generate(n, SEED, 0)
+    ores = o.solve(piv, 0)
+    assert ores.pivots == piv
+    assert all(p["objective"] == ores.objective for p in parts)
+    _check_against(parts, m, piv, o.get_log(), o.get_basis(), o.get_rows(m, 1)[0], lambda i: o.get_rows(i, 1)[0])
+    x0 = np.concatenate([p["x0"] for p in parts])
+    assert np.array_equal(x0, np.concatenate([o.get_rows(i0, 1024)[:, 0] for i0 in range(0, m, 1024)]))
+
+
+def test_config4_shape_two_processes_partition_invariance(lpg):
+    m, n, piv = 65536, 131072, 320
+    parts = _run(2, m, n, piv, {})
+    assert all(p["defer"] == 128 and p["wg"] == 0 for p in parts)     # 196,673 columns: the pair, 128-pivot blocks
+    # the same LP on one rank (run after the two processes have freed the GPU)
+    e = lpg.Engine(m, n + m + 1)
+    assert e.info.defer_k == 128
+    e.generate(n, SEED, lpg.GEN_DENSE)
+    e.reserve_log(piv + 8)
+    res = e.solve(piv, lpg.RULE_DANTZIG)
+    assert res.pivots == piv and all(p["objective"] == res.objective for p in parts)
+    _check_against(parts, m, piv, e.get_log(), e.get_basis(), e.get_rows(m, 1)[0], lambda i: e.get_rows(i, 1)[0])
+    assert np.array_equal(np.concatenate([p["x0"] for p in parts]), e.get_column0())
+    e.close()

@@ -189,6 +189,21 @@ def test_m_valued_cost_with_real_part():
 
 
 @needs_msplit
+@pytest.mark.gpu
+def test_m_valued_cost_ray_with_infeasible_rows():
+    """cost(x1) = M on `x2 >= 3, x2 <= 1` (no feasible point), x1 in no row: the
+    M row prices x1 first (ties with x2 go to the smaller column), whose column
+    is a ray while the artificial of `x2 >= 3` is still 3. A ray found with an
+    artificial left positive means INFEASIBLE, as lpg_solve_big_m reports it,
+    not UNBOUNDED."""
+    p = subprocess.run([MSPLIT, os.path.join(LP + "_extra", "m_ray_infeasible.txt"), "cost", "x1", "1", "1", "0"],
+                       capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert p.returncode == 0, p.stderr
+    assert "Big-M (symbolic M)" in p.stdout and "The LP is INFEASIBLE" in p.stdout and "valid=1" in p.stdout
+    assert "UNBOUNDED" not in p.stdout
+
+
+@needs_msplit
 @pytest.mark.parametrize("args", [["cell", "0", "x1"], ["cost-denominator", "x1"]])
 def test_m_where_it_cannot_be_kept_is_refused(args):
     """M in a constraint cell, or 1/M in a cost, cannot be held by the two
