@@ -249,7 +249,17 @@ __global__ __launch_bounds__(kBlock) void k_prep(double *__restrict__ T, Geo g, 
                                                  const Cand *__restrict__ cand, int ncand,
                                                  double *__restrict__ P, const double *__restrict__ Cs,
                                                  PricePart *__restrict__ pp, int *__restrict__ pc, Defer D) {
-    if (st->slot[s].status != RUNNING) return;
+    const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t nvec = (g.ncols + 1) / 2;
+    // with a communicator (!FUSE) an allreduce of P follows even when no pivot
+    // runs (the loop ended): send its identity, not the previous pivot's row
+    auto no_pivot = [&]() {
+        if (!FUSE && j2 < nvec) *(d2 *)(P + 2 * j2) = d2{-0.0, -0.0};
+    };
+    if (st->slot[s].status != RUNNING) {
+        no_pivot();
+        return;
+    }
     Cand best{0.0, 0.0, 0, -1};
     for (int q = threadIdx.x; q < ncand; q += kBlock) {
         const Cand c = cand[q];
@@ -264,6 +274,7 @@ __global__ __launch_bounds__(kBlock) void k_prep(double *__restrict__ T, Geo g, 
             st->slot[s].status = best.row < 0 ? UNBOUNDED : NUMERIC;
             st->slot[s].r = -1;
         }
+        no_pivot();
         return;
     }
     const int64_t rl = best.row - g.row0;
@@ -287,8 +298,6 @@ __global__ __launch_bounds__(kBlock) void k_prep(double *__restrict__ T, Geo g, 
         }
     }
     const double piv = best.piv;   // == T_t[r][k_t] (select_{t-1} computed and stored it)
-    const int64_t j2 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t nvec = (g.ncols + 1) / 2;
     d2 t = d2{0.0, 0.0};           // the pivot row as stored (issued before the staging barrier)
     if (own && j2 < nvec) t = *(const d2 *)(T + rl * g.ld + 2 * j2);
     __shared__ double s_c[LPG_DEFER_MAX];
@@ -694,7 +703,12 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
     const int64_t rqv = lane < D.q ? D.rq[lane] : -1;   // lane q of every wave holds r_q
     const int64_t rqv1 = TWO && 64 + lane < D.q ? D.rq[64 + lane] : -1;   // bank 1: r_{64 + lane}
     const int2 lj = col ? ((const int2 *)D.colmap)[j2] : int2{0, 0};   // logical indices of the two columns
-    if (status != RUNNING) return;
+    // MODE 1: the allreduce of P runs whether or not a pivot does (the loop
+    // may have ended): then every rank sends the identity, -0
+    if (status != RUNNING) {
+        if (MODE == 1 && col) *(d2 *)(P + 2 * j2) = d2{-0.0, -0.0};
+        return;
+    }
     if (MODE == 2 && !X.from_cand && !xch_gather<NT>(X, best)) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->slot[s].status = NUMERIC;
@@ -713,6 +727,7 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
             st->slot[s].status = best.row < 0 ? UNBOUNDED : NUMERIC;
             st->slot[s].r = -1;
         }
+        if (MODE == 1 && col) *(d2 *)(P + 2 * j2) = d2{-0.0, -0.0};
         return;
     }
     const bool own = !MR || (best.row >= g.row0 && best.row < g.row0 + g.nloc);   // uniform

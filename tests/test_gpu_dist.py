@@ -33,6 +33,7 @@ class ThreadComm:
         self.world = world
         self.bar = threading.Barrier(world)
         self.slots = [None] * world
+        self.violations = []
 
     def allgather(self, rank, data: bytes) -> bytes:
         self.slots[rank] = data
@@ -52,16 +53,22 @@ class ThreadComm:
         # buffer bit for bit (round 2 summed uninitialised padding here).
         bits = [np.ascontiguousarray(s).view(np.uint64) for s in self.slots]
         live = [q for q in range(self.world) if np.any(bits[q] << np.uint64(1))]
-        assert len(live) <= 1, f"ranks {live} both contributed to one exchange"
-        for q in range(self.world):
-            if q not in live:
-                assert np.all(bits[q] == bits[q][0]), f"rank {q} sent a mix of +0 and -0"
         acc = self.slots[0].copy()
         for q in range(1, self.world):
             acc = acc + self.slots[q]
+        bad = None
+        if len(live) > 1:
+            bad = f"ranks {live} both contributed to one exchange of {len(arr)} doubles"
+        for q in range(self.world):
+            if q not in live and not np.all(bits[q] == bits[q][0]):
+                bad = f"rank {q} sent a mix of +0 and -0"
         if live and all(bits[q][0] == np.uint64(1 << 63) for q in range(self.world) if q != live[0]):
-            assert np.array_equal(acc.view(np.uint64), bits[live[0]]), "the sum is not the owner's row"
+            if not np.array_equal(acc.view(np.uint64), bits[live[0]]):
+                bad = "the sum is not the owner's row"
         self.bar.wait()
+        if bad:
+            self.violations.append(bad)
+            raise AssertionError(bad)
         return acc
 
 
@@ -93,6 +100,7 @@ def _run_threads(lpg, world, m, n, seed, kind, rule, max_pivots, push=False):
         t.start()
     for t in th:
         t.join(600)
+    assert not comm.violations, comm.violations[:4]
     assert not errs, errs
     return out
 
