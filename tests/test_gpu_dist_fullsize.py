@@ -20,7 +20,8 @@ process per GPU), at the full sizes:
     failing (round 2).
 * config 4's shape (65536 x 131072, 32768 rows and 51.5 GB per rank, blocks
   of 128 pivots, the multi-rank column trade over 196,609 columns), 320
-  pivots: bitwise equal to the single-rank engine (partition invariance: log,
+  pivots over the collectives (the owner push's spinning prep grid needs a GPU
+  per rank at this size, see the test): bitwise equal to the single-rank engine (partition invariance: log,
   basis, objective row, column 0, every pivot row and 64 sampled rows per
   rank), plus unit basic columns on those rows and b >= 0 on every row.
 
@@ -57,7 +58,7 @@ def _sample(m, world, rank, k, seed):
     return sorted(set(rng.choice(np.arange(r0, r1), k, replace=False).tolist()) | {r0, r1 - 1})
 
 
-def _worker(rank, world, port, m, n, seed, pivots, outdir, env):
+def _worker(rank, world, port, m, n, seed, pivots, outdir, env, push):
     os.environ.update(env)
     import torch
     import torch.distributed as dist
@@ -79,8 +80,9 @@ def _worker(rank, world, port, m, n, seed, pivots, outdir, env):
 
     e = lpg.Engine(m, n + m + 1, world=world, rank=rank)
     e.comm_init_host(allgather, allreduce)
-    h = allgather(e.push_handle())
-    e.comm_init_push([h[64 * r:64 * r + 64] for r in range(world)])
+    if push:
+        h = allgather(e.push_handle())
+        e.comm_init_push([h[64 * r:64 * r + 64] for r in range(world)])
     wg0 = e.info.pivot_wg
     e.generate(n, seed, lpg.GEN_DENSE)
     e.reserve_log(pivots + 8)
@@ -99,14 +101,14 @@ def _worker(rank, world, port, m, n, seed, pivots, outdir, env):
     dist.destroy_process_group()
 
 
-def _run(world, m, n, pivots, env):
+def _run(world, m, n, pivots, env, push=True):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, port, m, n, SEED, pivots, d, env), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, port, m, n, SEED, pivots, d, env, push), nprocs=world, join=True)
         return [pickle.load(open(os.path.join(d, f"r{q}.pkl"), "rb")) for q in range(world)]
 
 
@@ -152,8 +154,12 @@ def test_config3_two_processes_bitwise(lpg, mr):
 
 def test_config4_shape_two_processes_partition_invariance(lpg):
     m, n, piv = 65536, 131072, 320
-    parts = _run(2, m, n, piv, {})
-    assert all(p["defer"] == 128 and p["wg"] == 0 for p in parts)     # 196,673 columns: the pair, 128-pivot blocks
+    # the collectives (host transport), not the owner push: on ONE GPU the push's
+    # non-owner prep blocks spin until the owner's chunk lands, and a 385-block
+    # spinning grid can hold every slot the owner's grid needs (one process per
+    # GPU, the real layout, has no such coupling); config 3's 97-block grids fit
+    parts = _run(2, m, n, piv, {}, push=False)
+    assert all(p["defer"] == 128 and p["wg"] == 0 and p["exchange"] == 0 for p in parts)   # the pair, 128-pivot blocks
     # the same LP on one rank (run after the two processes have freed the GPU)
     e = lpg.Engine(m, n + m + 1)
     assert e.info.defer_k == 128
