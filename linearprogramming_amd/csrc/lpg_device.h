@@ -16,21 +16,44 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 // reductions: 64-lane wave shuffles, then the 4 waves through LDS
 // ------------------------------------------------------------------------
 
+// Keeping the better of several structs ("if (better(c, best)) best = c")
+// is MISCOMPILED by hipcc (ROCm 7.2, gfx950) when `better` is written with
+// early returns: the structurizer turns the nested conditions into exec-mask
+// regions, and in the path "best valid -> compare" it parks best's old field
+// in the very register that holds the new candidate's field, so a candidate
+// that wins keeps some of best's old fields. Seen twice: the pad field of
+// k_price's partials (round 1), and k_prep_d's gathered ratio candidates at
+// config 4 over 2 ranks (2 x 129 candidates, 2 per thread): row 65436 of one
+// candidate paired with the pivot element of another, so P was divided by
+// the wrong number (tools/diag_mr4.py; the ISA showed `v_mov_b64 v[4:5],
+// v[68:69]` overwriting the loaded piv before the conditional copy). So the
+// comparisons below are branch-free (bitwise & |, selects) and every "take"
+// is a per-field select on ONE predicate (cand_take / pp_take).
 __device__ __forceinline__ bool cand_better(const Cand &a, const Cand &b) {
-    if (a.row < 0) return false;
-    if (b.row < 0) return true;
-    if (a.theta != b.theta) return a.theta < b.theta;
-    return a.key < b.key;
+    const bool ord = (a.theta != b.theta) ? (a.theta < b.theta) : (a.key < b.key);
+    return (a.row >= 0) & ((b.row < 0) | ord);
 }
 
 template <int RULE>
 __device__ __forceinline__ bool pp_better(const PricePart &a, const PricePart &b) {
-    if (a.j < 0) return false;
-    if (b.j < 0) return true;
-    if (RULE == RULE_BLAND) return a.j < b.j;
-    if (a.cls != b.cls) return a.cls < b.cls;
-    if (a.v != b.v) return a.v < b.v;
-    return a.j < b.j;
+    bool ord;
+    if (RULE == RULE_BLAND) ord = a.j < b.j;
+    else ord = (a.cls != b.cls) ? (a.cls < b.cls) : ((a.v != b.v) ? (a.v < b.v) : (a.j < b.j));
+    return (a.j >= 0) & ((b.j < 0) | ord);
+}
+
+__device__ __forceinline__ void cand_take(Cand &best, const Cand &c, bool t) {
+    best.theta = t ? c.theta : best.theta;
+    best.piv = t ? c.piv : best.piv;
+    best.key = t ? c.key : best.key;
+    best.row = t ? c.row : best.row;
+}
+
+__device__ __forceinline__ void pp_take(PricePart &best, const PricePart &c, bool t) {
+    best.v = t ? c.v : best.v;
+    best.j = t ? c.j : best.j;
+    best.cls = t ? c.cls : best.cls;
+    best.pad = t ? c.pad : best.pad;
 }
 
 __device__ __forceinline__ Cand shfl_xor_cand(const Cand &c, int mask) {
@@ -57,7 +80,7 @@ inline __device__ Cand block_reduce_cand(Cand c) {
 #pragma unroll
     for (int mask = 32; mask > 0; mask >>= 1) {
         Cand o = shfl_xor_cand(c, mask);
-        if (cand_better(o, c)) c = o;
+        cand_take(c, o, cand_better(o, c));
     }
     const int w = threadIdx.x >> 6;
     __syncthreads();
@@ -66,7 +89,7 @@ inline __device__ Cand block_reduce_cand(Cand c) {
     Cand b = sh[0];
 #pragma unroll
     for (int i = 1; i < kBlock / 64; i++)
-        if (cand_better(sh[i], b)) b = sh[i];
+        cand_take(b, sh[i], cand_better(sh[i], b));
     return b;
 }
 
@@ -76,7 +99,7 @@ __device__ PricePart block_reduce_pp(PricePart p) {
 #pragma unroll
     for (int mask = 32; mask > 0; mask >>= 1) {
         PricePart o = shfl_xor_pp(p, mask);
-        if (pp_better<RULE>(o, p)) p = o;
+        pp_take(p, o, pp_better<RULE>(o, p));
     }
     const int w = threadIdx.x >> 6;
     __syncthreads();
@@ -85,7 +108,7 @@ __device__ PricePart block_reduce_pp(PricePart p) {
     PricePart b = sh[0];
 #pragma unroll
     for (int i = 1; i < kBlock / 64; i++)
-        if (pp_better<RULE>(sh[i], b)) b = sh[i];
+        pp_take(b, sh[i], pp_better<RULE>(sh[i], b));
     return b;
 }
 
@@ -285,7 +308,7 @@ __device__ __forceinline__ void price_one(PricePart &best, double dM, double dR,
     } else {
         return;
     }
-    if (pp_better<RULE>(c, best)) best = c;
+    pp_take(best, c, pp_better<RULE>(c, best));
 }
 
 // ---- owner-push exchange (Xch, lpg_internal.h) ----

@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void k_price(double *__restrict__ T, Geo g,
         price_one<RULE>(best, dM.y, dR.y, lj.y, g);
     }
     if (MODE == 1) count_live(pc, live);
-    best = block_reduce_pp<RULE>(best);
+    best = block_argmin_pp<RULE>(best);   // unique keys: no struct selects (see below)
     // pad (the physical column) == j in caller order. Set it here: hipcc
     // (ROCm 7.2) miscompiled the pad field of the inlined price_one's
     // "if (better) best = c" in this kernel (pad kept the previous best's
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(kBlock) void k_prep(double *__restrict__ T, Geo g, 
     Cand best{0.0, 0.0, 0, -1};
     for (int q = threadIdx.x; q < ncand; q += kBlock) {
         const Cand c = cand[q];
-        if (cand_better(c, best)) best = c;
+        cand_take(best, c, cand_better(c, best));
     }
     best = block_reduce_cand(best);
     // the oracle's rule (oracle/lpo.c lpo_solve): NUMERIC iff the pivot element or
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
     } else {
         for (int q = threadIdx.x; q < npp; q += kBlock) {
             const PricePart c = pp[q];
-            if (pp_better<RULE>(c, pb)) pb = c;
+            pp_take(pb, c, pp_better<RULE>(c, pb));
         }
         pb = block_reduce_pp<RULE>(pb);
     }
@@ -553,7 +553,7 @@ __global__ __launch_bounds__(kBlock) void k_select(const double *__restrict__ T,
             c.piv = isfinite(b) ? a : __longlong_as_double(0x7ff8000000000000ll);   // b_r not finite: NUMERIC at prep
             c.row = grow;
             c.key = RULE == RULE_BLAND ? (grow == r ? kc : basis[grow]) : grow;
-            if (cand_better(c, best)) best = c;
+            cand_take(best, c, cand_better(c, best));
         }
     }
     best = block_reduce_cand(best);
@@ -636,7 +636,7 @@ __device__ bool xch_gather(const Xch &X, Cand &best) {
             c.piv = __longlong_as_double((long long)(((v[3] & 0xffffffffull) << 32) | (v[2] & 0xffffffffull)));
             c.key = (int64_t)(int32_t)(uint32_t)v[4];
             c.row = (int64_t)(int32_t)(uint32_t)v[5];
-            if (cand_better(c, b)) b = c;
+            cand_take(b, c, cand_better(c, b));
         }
         if (__syncthreads_and(ok)) {
             best = b;
@@ -674,7 +674,7 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
     if (MODE != 2 || X.from_cand) {
         for (int q = threadIdx.x; q < ncand; q += NT) {
             const Cand c = cand[q];
-            if (cand_better(c, best)) best = c;
+            cand_take(best, c, cand_better(c, best));
         }
     }
     d2 dM = d2{0.0, 0.0}, dR = d2{0.0, 0.0};
@@ -909,7 +909,7 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
     PricePart pb{0.0, -1, 0, 0};
     for (int q = threadIdx.x; q < npp; q += NT) {
         const PricePart c = pp[q];
-        if (pp_better<RULE>(c, pb)) pb = c;
+        pp_take(pb, c, pp_better<RULE>(c, pb));
     }
     double ob = 0.0, csi = 0.0;
     if (row) {
@@ -1059,7 +1059,7 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
             c.piv = isfinite(b) ? a : __longlong_as_double(0x7ff8000000000000ll);   // b_r not finite: NUMERIC at prep
             c.row = grow;
             c.key = RULE == RULE_BLAND ? (grow == r ? kc : bkey) : grow;
-            if (cand_better(c, best)) best = c;
+            cand_take(best, c, cand_better(c, best));
         }
     }
     LPG_PH(1, 4);
@@ -1282,7 +1282,7 @@ __device__ __forceinline__ void dual_row_cand(Cand &best, double b, int64_t grow
     c.piv = 0.0;
     c.key = grow;
     c.row = grow;
-    if (cand_better(c, best)) best = c;
+    cand_take(best, c, cand_better(c, best));
 }
 
 __global__ __launch_bounds__(kBlock) void k_dual_rows(const double *__restrict__ T, Geo g, Cand *__restrict__ part) {
@@ -1300,7 +1300,7 @@ __global__ __launch_bounds__(kBlock) void k_dual_price(const double *__restrict_
     Cand best{0.0, 0.0, 0, -1};
     for (int q = threadIdx.x; q < npart; q += kBlock) {
         const Cand c = part[q];
-        if (cand_better(c, best)) best = c;
+        cand_take(best, c, cand_better(c, best));
     }
     best = block_reduce_cand(best);
     if (best.row < 0) {                      // primal feasible: optimal
@@ -1333,7 +1333,7 @@ __global__ __launch_bounds__(kBlock) void k_dual_price(const double *__restrict_
             c.j = j;
             c.cls = 0;
             c.pad = 0;
-            if (pp_better<RULE_DANTZIG>(c, pb)) pb = c;
+            pp_take(pb, c, pp_better<RULE_DANTZIG>(c, pb));
         }
     }
     count_live(pc, live);
@@ -1359,7 +1359,7 @@ __global__ __launch_bounds__(kBlock) void k_dual_prep(const double *__restrict__
     PricePart pb{0.0, -1, 0, 0};
     for (int q = threadIdx.x; q < npp; q += kBlock) {
         const PricePart c = pp[q];
-        if (pp_better<RULE_DANTZIG>(c, pb)) pb = c;
+        pp_take(pb, c, pp_better<RULE_DANTZIG>(c, pb));
     }
     pb = block_reduce_pp<RULE_DANTZIG>(pb);
     if (pb.j < 0) {                          // no a_rj < 0: the LP is primal infeasible

@@ -166,7 +166,13 @@ def test_config4_shape_two_processes_partition_invariance(lpg):
     e.generate(n, SEED, lpg.GEN_DENSE)
     e.reserve_log(piv + 8)
     res = e.solve(piv, lpg.RULE_DANTZIG)
-    assert res.pivots == piv and all(p["objective"] == res.objective for p in parts)
+    k1, r1 = e.get_log()
+    for p in parts:                                  # the first divergence, if any, named before the details
+        k2, r2 = p["log"]
+        bad = np.nonzero((k1[:len(k2)] != k2[:len(k1)]) | (r1[:len(k2)] != r2[:len(k1)]))[0]
+        assert len(bad) == 0, f"pivot {bad[0]}: single rank ({k1[bad[0]]}, {r1[bad[0]]}), rank ({k2[bad[0]]}, {r2[bad[0]]})"
+    assert res.pivots == piv and all(p["objective"] == res.objective for p in parts), \
+        (res.objective, [p["objective"] for p in parts])
     _check_against(parts, m, piv, e.get_log(), e.get_basis(), e.get_rows(m, 1)[0], lambda i: e.get_rows(i, 1)[0])
     assert np.array_equal(np.concatenate([p["x0"] for p in parts]), e.get_column0())
     e.close()
