@@ -13,16 +13,27 @@
  *   lpgcli --lp MODEL [--big-m] [--rule ...]     the reference's model format,
  *          through the C front end (lpfront.c) onto the device
  *   lpgcli --lp-dump MODEL                       the SimplexMatrix as JSON (no device)
+ *   lpgcli --synthetic M N --gpus P [--exchange push|host]
+ *          the row partition over P ranks, one process each (forked before
+ *          any HIP call; the parent only relays the host-staged collectives
+ *          over socketpairs and never touches a GPU); rank r on device
+ *          (D + r) mod #devices; rank 0 prints the JSON line
  *
  * FILE: "m ncols" then m+1 rows of ncols numbers ([b | a_1..a_N], objective
  * row last, d_j = z_j - c_j), then m basic columns (1-based).
  */
 #define _POSIX_C_SOURCE 200809L
+#include <errno.h>
+#include <signal.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/socket.h>
+#include <sys/types.h>
+#include <sys/wait.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "lpfront.h"
 #include "lpg.h"
@@ -40,9 +51,226 @@ static const char *status_name(int s) {
 
 static int usage(const char *argv0) {
     fprintf(stderr, "Usage:\n\t%s --synthetic M N [--seed S] [--kind dense|degenerate] [--rule dantzig|bland]"
-                    " [--pivots K] [--device D]\n\t%s --tableau FILE [--rule dantzig|bland] [--pivots K]\n",
-            argv0, argv0);
+                    " [--pivots K] [--device D] [--gpus P [--exchange push|host]]\n"
+                    "\t%s --tableau FILE [--rule dantzig|bland] [--pivots K]\n"
+                    "\t%s --lp MODEL [--big-m] [--rule dantzig|bland]\n\t%s --lp-dump MODEL\n",
+            argv0, argv0, argv0, argv0);
     return 2;
+}
+
+/* FNV-1a over the pivot log (k, r pairs): one number to compare runs by */
+static uint64_t log_fnv(lpg_ctx *ctx, int64_t npiv) {
+    uint64_t h = 1469598103934665603ull;
+    if (npiv <= 0) return h;
+    int64_t *k = (int64_t *)malloc((size_t)npiv * sizeof(int64_t)), *r = (int64_t *)malloc((size_t)npiv * sizeof(int64_t));
+    const int64_t n = (k && r) ? lpg_get_log(ctx, k, r, npiv) : 0;
+    for (int64_t q = 0; q < n && q < npiv; q++) {
+        const int64_t v[2] = {k[q], r[q]};
+        const unsigned char *b = (const unsigned char *)v;
+        for (size_t i = 0; i < sizeof v; i++) h = (h ^ b[i]) * 1099511628211ull;
+    }
+    free(k);
+    free(r);
+    return h;
+}
+
+/* ---- --gpus P: the row partition from plain C ----------------------------
+ * The reference host is one process (Source/main.c:4-45); the north star's
+ * row partition wants one process per GPU. The parent forks P ranks before
+ * any HIP call (no process ever forks or execs after GPU initialisation) and
+ * then only relays the collectives the engine's setup and bootstraps need
+ * (lpg_host_comm_ops: allgather, allreduce of doubles) over one socketpair
+ * per rank; per pivot the ranks talk through the owner-push exchange
+ * (IPC-mapped device buffers, --exchange push, the default) or through these
+ * host collectives (--exchange host). Rank r uses device (D + r) mod
+ * #devices, so P ranks may share one GPU. */
+typedef struct {
+    int fd, world, rank;
+} hub_link;
+
+static int write_all(int fd, const void *p, size_t n) {
+    const char *c = (const char *)p;
+    while (n > 0) {
+        const ssize_t w = write(fd, c, n);
+        if (w < 0 && errno == EINTR) continue;
+        if (w <= 0) return -1;
+        c += w;
+        n -= (size_t)w;
+    }
+    return 0;
+}
+
+static int read_fd(int fd, void *p, size_t n) {
+    char *c = (char *)p;
+    while (n > 0) {
+        const ssize_t r = read(fd, c, n);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return -1;
+        c += r;
+        n -= (size_t)r;
+    }
+    return 0;
+}
+
+/* one collective: op ('G' allgather, 'R' allreduce f64) and the payload up, the result down */
+static int hub_call(hub_link *h, char op, const void *send, size_t bytes, void *recv, size_t rbytes) {
+    const uint64_t n = bytes;
+    if (write_all(h->fd, &op, 1) || write_all(h->fd, &n, sizeof n) || write_all(h->fd, send, bytes)) return -1;
+    return read_fd(h->fd, recv, rbytes);
+}
+
+static int cb_allgather(void *user, const void *send, void *recv, size_t bytes) {
+    hub_link *h = (hub_link *)user;
+    return hub_call(h, 'G', send, bytes, recv, bytes * (size_t)h->world);
+}
+
+static int cb_allreduce(void *user, double *buf, size_t count) {
+    return hub_call((hub_link *)user, 'R', buf, count * sizeof(double), buf, count * sizeof(double));
+}
+
+/* the parent: serve collectives until every rank has hung up; sums in rank order */
+static int hub_serve(int world, const int *fds) {
+    char **in = (char **)calloc((size_t)world, sizeof(char *));
+    int rc = 0;
+    for (;;) {
+        char op0 = 0;
+        uint64_t n0 = 0;
+        int eof = 0;
+        for (int r = 0; r < world; r++) {
+            char op = 0;
+            uint64_t n = 0;
+            if (read_fd(fds[r], &op, 1) || read_fd(fds[r], &n, sizeof n)) {
+                eof++;
+                continue;
+            }
+            if (r == 0 || eof) {
+                op0 = op;
+                n0 = n;
+            }
+            if (op != op0 || n != n0 || (op != 'G' && op != 'R') || (op == 'R' && n % 8)) {
+                fprintf(stderr, "ERROR: lpgcli --gpus: ranks disagree on a collective\n");
+                rc = 1;
+                goto done;
+            }
+            free(in[r]);
+            in[r] = (char *)malloc(n ? n : 1);
+            if (!in[r] || read_fd(fds[r], in[r], n)) {
+                rc = 1;
+                goto done;
+            }
+        }
+        if (eof == world) break;                /* every rank finished */
+        if (eof) {                              /* a rank left inside a collective: end them all */
+            fprintf(stderr, "ERROR: lpgcli --gpus: a rank exited during a collective\n");
+            rc = 1;
+            goto done;
+        }
+        if (op0 == 'G') {
+            for (int r = 0; r < world; r++)
+                for (int q = 0; q < world; q++)
+                    if (write_all(fds[r], in[q], n0)) { rc = 1; goto done; }
+        } else {
+            double *acc = (double *)in[0];
+            for (int q = 1; q < world; q++)
+                for (uint64_t i = 0; i < n0 / 8; i++) acc[i] += ((double *)in[q])[i];
+            for (int r = 0; r < world; r++)
+                if (write_all(fds[r], acc, n0)) { rc = 1; goto done; }
+        }
+    }
+done:
+    for (int r = 0; r < world; r++) {
+        free(in[r]);
+        close(fds[r]);
+    }
+    free(in);
+    return rc;
+}
+
+typedef struct {
+    long long m, n, pivots;
+    unsigned long long seed;
+    int kind, rule, device, world, push;
+} dist_args;
+
+static int run_rank(const dist_args *a, int rank, int fd) {
+    hub_link h = {fd, a->world, rank};
+    int count = 0, rc;
+    lpg_ctx *ctx = NULL;
+    if (lpg_device_count(&count) != 0 || count < 1) {
+        fprintf(stderr, "ERROR: rank %d: no GPU\n", rank);
+        return 1;
+    }
+    const int dev = (a->device + rank) % count;
+    lpg_host_comm_ops ops = {&h, cb_allgather, cb_allreduce};
+    if ((rc = lpg_create_dist(&ctx, dev, a->world, rank, a->m, a->n + a->m + 1, 0)) != 0 ||
+        (rc = lpg_comm_init_host(ctx, &ops)) != 0)
+        goto fail;
+    if (a->push) {
+        char mine[LPG_PUSH_HANDLE_BYTES];
+        char *all = (char *)malloc((size_t)a->world * LPG_PUSH_HANDLE_BYTES);
+        rc = all ? lpg_comm_push_handle(ctx, mine, sizeof mine) : LPG_ERR_OOM;
+        if (!rc) rc = cb_allgather(&h, mine, all, sizeof mine) ? LPG_ERR_COMM : 0;
+        if (!rc) rc = lpg_comm_init_push(ctx, all, (size_t)a->world * LPG_PUSH_HANDLE_BYTES);
+        free(all);
+        if (rc) goto fail;
+    }
+    if ((rc = lpg_generate(ctx, a->n, a->seed, a->kind)) != 0) goto fail;
+    char one = 1, got[256];
+    if (a->world > 256 || cb_allgather(&h, &one, got, 1)) goto fail;   /* start together */
+    const double t0 = now();
+    lpg_result res;
+    if ((rc = lpg_solve(ctx, a->pivots, a->rule, &res)) != 0) goto fail;
+    if (cb_allgather(&h, &one, got, 1)) goto fail;                     /* the slowest rank's end */
+    const double dt = now() - t0;
+    lpg_info_t info;
+    lpg_info(ctx, &info);
+    const uint64_t fnv = log_fnv(ctx, res.pivots);
+    if (rank == 0)
+        printf("{\"status\": \"%s\", \"pivots\": %lld, \"objective\": %.17g, \"seconds\": %.6f, "
+               "\"pivots_per_s\": %.3f, \"m\": %lld, \"ncols\": %lld, \"rule\": \"%s\", \"gpus\": %d, "
+               "\"exchange\": %d, \"pivot_wg\": %d, \"residency_fallbacks\": %d, \"defer_k\": %d, "
+               "\"log_fnv\": \"%016llx\"}\n",
+               status_name(res.status), (long long)res.pivots, res.objective, dt, dt > 0 ? (double)res.pivots / dt : 0.0,
+               (long long)info.m, (long long)info.ncols, a->rule == LPG_RULE_BLAND ? "bland" : "dantzig", a->world,
+               info.exchange, info.pivot_wg, info.residency_fallbacks, info.defer_k, (unsigned long long)fnv);
+    fflush(stdout);
+    lpg_destroy(ctx);
+    close(fd);
+    return 0;
+fail:
+    fprintf(stderr, "ERROR: rank %d: %s\n", rank, lpg_last_error(ctx));
+    lpg_destroy(ctx);
+    close(fd);
+    return 1;
+}
+
+static int run_dist(const dist_args *a) {
+    int *fds = (int *)calloc((size_t)a->world, sizeof(int));
+    pid_t *pid = (pid_t *)calloc((size_t)a->world, sizeof(pid_t));
+    if (!fds || !pid) return 1;
+    fflush(stdout);
+    for (int r = 0; r < a->world; r++) {
+        int sv[2];
+        if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) return 1;
+        pid[r] = fork();
+        if (pid[r] < 0) return 1;
+        if (pid[r] == 0) {                      /* rank r: no HIP call happened in this process yet */
+            close(sv[0]);
+            for (int q = 0; q < r; q++) close(fds[q]);
+            _exit(run_rank(a, r, sv[1]));
+        }
+        close(sv[1]);
+        fds[r] = sv[0];
+    }
+    int rc = hub_serve(a->world, fds);
+    for (int r = 0; r < a->world; r++) {
+        int st = 0;
+        if (rc) kill(pid[r], SIGTERM);
+        if (waitpid(pid[r], &st, 0) < 0 || !WIFEXITED(st) || WEXITSTATUS(st) != 0) rc = 1;
+    }
+    free(fds);
+    free(pid);
+    return rc;
 }
 
 static char *read_all(const char *path) {
@@ -198,7 +426,7 @@ static int load_tableau_file(lpg_ctx **ctx, const char *path, int device) {
 int main(int argc, char **argv) {
     long long m = 0, n = 0, pivots = (long long)1 << 40;
     unsigned long long seed = 20220518ull;
-    int kind = LPG_GEN_DENSE, rule = LPG_RULE_DANTZIG, device = 0;
+    int kind = LPG_GEN_DENSE, rule = LPG_RULE_DANTZIG, device = 0, gpus = 1, push = 1;
     const char *file = NULL, *lpfile = NULL;
     int dump = 0, bigm = 0;
     for (int a = 1; a < argc; a++) {
@@ -222,11 +450,20 @@ int main(int argc, char **argv) {
             pivots = atoll(argv[++a]);
         } else if (!strcmp(argv[a], "--device") && a + 1 < argc) {
             device = atoi(argv[++a]);
+        } else if (!strcmp(argv[a], "--gpus") && a + 1 < argc) {
+            gpus = atoi(argv[++a]);
+        } else if (!strcmp(argv[a], "--exchange") && a + 1 < argc) {
+            push = strcmp(argv[++a], "host") != 0;
         } else {
             return usage(argv[0]);
         }
     }
     if (lpfile) return run_lp(lpfile, dump, bigm, rule, device);
+    if (gpus > 1) {
+        if (!(m > 0 && n > 0) || gpus > m || gpus > 64) return usage(argv[0]);
+        const dist_args da = {m, n, pivots, seed, kind, rule, device, gpus, push};
+        return run_dist(&da);
+    }
     lpg_ctx *ctx = NULL;
     int rc;
     if (file) {
@@ -255,9 +492,11 @@ int main(int argc, char **argv) {
     lpg_info_t info;
     lpg_info(ctx, &info);
     printf("{\"status\": \"%s\", \"pivots\": %lld, \"objective\": %.17g, \"seconds\": %.6f, "
-           "\"pivots_per_s\": %.3f, \"m\": %lld, \"ncols\": %lld, \"rule\": \"%s\"}\n",
+           "\"pivots_per_s\": %.3f, \"m\": %lld, \"ncols\": %lld, \"rule\": \"%s\", \"gpus\": 1, "
+           "\"defer_k\": %d, \"log_fnv\": \"%016llx\"}\n",
            status_name(res.status), (long long)res.pivots, res.objective, dt, dt > 0 ? (double)res.pivots / dt : 0.0,
-           (long long)info.m, (long long)info.ncols, rule == LPG_RULE_BLAND ? "bland" : "dantzig");
+           (long long)info.m, (long long)info.ncols, rule == LPG_RULE_BLAND ? "bland" : "dantzig", info.defer_k,
+           (unsigned long long)log_fnv(ctx, res.pivots));
     lpg_destroy(ctx);
     return 0;
 }

@@ -1,0 +1,97 @@
+"""host/lpgcli: the plain-C host (north star: "the host stays plain C") on
+the device, single rank and row-partitioned over P processes (--gpus P).
+
+The reference host is one interactive process (Source/main.c:4-45); lpgcli is
+its non-interactive counterpart (SURVEY.md §5 config / flags). --gpus P forks
+P ranks before any HIP call; the parent relays the host-staged collectives
+over socketpairs and never touches the GPU. On the one-GPU box all ranks
+share the card (rank r -> device r mod 1), the layout the row partition
+tests use; the 8-GPU node gives each its own.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle.lpo import Oracle
+
+CLI = os.path.join(ROOT, "host", "lpgcli")
+needs_cli = pytest.mark.skipif(not os.path.exists(CLI), reason="host/lpgcli not built")
+
+
+def _fnv(k, r):
+    h = 1469598103934665603
+    for a, b in zip(k.tolist(), r.tolist()):
+        for byte in np.array([a, b], dtype=np.int64).tobytes():
+            h = ((h ^ byte) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return f"{h:016x}"
+
+
+def _cli(args, env=None, timeout=300):
+    p = subprocess.run([CLI] + args, capture_output=True, text=True, timeout=timeout,
+                       env={**os.environ, **(env or {})})
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    return p, lines
+
+
+@needs_cli
+def test_gpus_without_a_device_fails_cleanly():
+    """Every rank fails (no GPU in the build container, or a bad device): the
+    hub sees them all hang up, nothing blocks, the exit status is non-zero."""
+    if os.environ.get("HIP_VISIBLE_DEVICES") is None and os.path.exists("/dev/kfd"):
+        pytest.skip("a GPU is visible: the GPU tests below cover --gpus")
+    p, lines = _cli(["--synthetic", "64", "64", "--gpus", "3"], timeout=60)
+    assert p.returncode != 0 and not lines
+    assert "ERROR: rank" in p.stderr
+
+
+@needs_cli
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,gpus,extra,env", [
+    (1024, 2048, 2, [], {}),                                  # owner push, persistent launch on every rank
+    (1024, 2048, 2, [], {"LPG_PERSIST_MR": "0"}),            # owner push, the two-kernel pair
+    (1024, 2048, 2, ["--exchange", "host"], {}),             # the host collectives every pivot
+    (701, 903, 3, [], {}),                                    # uneven row blocks
+    (300, 500, 2, ["--kind", "degenerate", "--rule", "bland"], {}),
+])
+def test_gpus_equals_one_rank_and_the_oracle(m, n, gpus, extra, env):
+    p1, l1 = _cli(["--synthetic", str(m), str(n)] + extra, env)
+    assert p1.returncode == 0, p1.stderr
+    one = json.loads(l1[-1])
+    pp, lp = _cli(["--synthetic", str(m), str(n), "--gpus", str(gpus)] + extra, env)
+    assert pp.returncode == 0, pp.stderr
+    assert len(lp) == 1, lp                      # rank 0 alone prints, one JSON line
+    dist = json.loads(lp[0])
+    assert dist["gpus"] == gpus and dist["status"] == one["status"] == "OPTIMAL"
+    assert dist["pivots"] == one["pivots"] and dist["objective"] == one["objective"]
+    assert dist["log_fnv"] == one["log_fnv"]
+    assert (dist["exchange"] == 0) if "host" in extra else (dist["exchange"] in (1, 2))
+    kind = 1 if "degenerate" in extra else 0
+    o = Oracle(m, n + m + 1)
+    o.generate(n, 20220518, kind)
+    res = o.solve(1 << 40, 1 if "bland" in extra else 0)
+    assert res.pivots == one["pivots"] and res.objective == one["objective"]
+    assert _fnv(*o.get_log()) == one["log_fnv"]
+
+
+@needs_cli
+@pytest.mark.gpu
+def test_gpus_config3_pair_path():
+    """BASELINE config 3 from plain C over 2 processes on the one GPU with the
+    pair (persistent launches of both ranks do not fit one GPU at once),
+    200 pivots: the single-rank log, objective and pivot count."""
+    args = ["--synthetic", "16384", "32768", "--pivots", "200"]
+    p1, l1 = _cli(args, timeout=600)
+    assert p1.returncode == 0, p1.stderr
+    one = json.loads(l1[-1])
+    pp, lp = _cli(args + ["--gpus", "2"], {"LPG_PERSIST_MR": "0"}, timeout=600)
+    assert pp.returncode == 0, pp.stderr
+    assert len(lp) == 1
+    dist = json.loads(lp[0])
+    assert dist["pivots"] == one["pivots"] == 200 and dist["objective"] == one["objective"]
+    assert dist["log_fnv"] == one["log_fnv"] and dist["pivot_wg"] == 0
