@@ -72,50 +72,138 @@ static void afree_all(Ctx *c) {
     c->head.next = NULL;
 }
 
-/* ---- rationals (numOprts.c; long overflow -> invalid, approximated by int64 range) ---- */
+/* ---- rationals: the reference's `long` arithmetic, operation for operation --
+ * The reference keeps every coefficient as a pair of C `long`s and guards
+ * products and sums with checks that rely on wrap-around (numOprts.c:19-26,
+ * 37-129; basicFuncs.c:123-158), built here at -O0 -fwrapv (oracle/Makefile).
+ * These helpers redo each of its steps in int64 with explicit two's-complement
+ * wrap, so a value the reference's checks reject (an intermediate product or
+ * sum that wraps, though the reduced result would fit) is rejected here too,
+ * and an invalid value keeps the numerator and denominator the reference
+ * keeps (a later sum may use them). Where the reference's own arithmetic
+ * traps -- x / 0 or LONG_MIN / -1 is SIGFPE on x86-64 -- the model is
+ * refused with a message instead (tests/test_frontend.py records these). */
 
 typedef struct {
     lpf_q q;
     int valid;
 } Num;
 
-static int64_t gcd64(int64_t a, int64_t b) {
-    a = a < 0 ? -a : a;
-    b = b < 0 ? -b : b;
+static int64_t w_mul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+static int64_t w_neg(int64_t a) { return (int64_t)(0 - (uint64_t)a); }
+static int64_t w_labs(int64_t a) { return a < 0 ? w_neg(a) : a; }   /* labs(LONG_MIN) == LONG_MIN */
+
+static int64_t c_div(Ctx *c, int64_t a, int64_t b) {
+    if (b == 0 || (a == INT64_MIN && b == -1)) die(c, "ERROR: arithmetic trap (the reference dies with SIGFPE here)");
+    return a / b;
+}
+static int64_t c_mod(Ctx *c, int64_t a, int64_t b) {
+    if (b == 0 || (a == INT64_MIN && b == -1)) die(c, "ERROR: arithmetic trap (the reference dies with SIGFPE here)");
+    return a % b;
+}
+
+/* GCD, basicFuncs.c:123-137 */
+static int64_t ref_gcd(Ctx *c, int64_t a, int64_t b) {
+    a = w_labs(a);
+    b = w_labs(b);
+    if (b > a) {
+        const int64_t t = b;
+        b = a;
+        a = t;
+    }
     while (b) {
-        int64_t t = a % b;
-        a = b;
-        b = t;
+        const int64_t t = b;
+        b = c_mod(c, a, b);
+        a = t;
     }
     return a;
 }
 
-static Num mk(Ctx *c, __int128 n, __int128 d) {
-    if (d < 0) n = -n, d = -d;
-    __int128 a = n < 0 ? -n : n, b = d;
-    while (b) {
-        __int128 t = a % b;
-        a = b;
-        b = t;
-    }
-    if (a > 1) n /= a, d /= a;
-    const __int128 lim = (__int128)1 << 63;
-    if (n >= lim || -n >= lim || d >= lim) die(c, "WARNING: operation overflowed");
-    Num r = {{(int64_t)n, (int64_t)d}, 1};
+/* LCM, basicFuncs.c:145-158: -1 when the product wraps */
+static int64_t ref_lcm(Ctx *c, int64_t a, int64_t b) {
+    const int64_t d = ref_gcd(c, a, b);
+    a = w_labs(a);
+    b = w_labs(b);
+    const int64_t q = c_div(c, a, d), r = w_mul(q, b);
+    if (q != 0 && c_div(c, r, q) != b) return -1;
     return r;
 }
 
-static Num add(Ctx *c, Num a, Num b) {
-    if (!a.valid || !b.valid) return (Num){{0, 0}, 0};
-    return mk(c, (__int128)a.q.num * b.q.den + (__int128)b.q.num * a.q.den, (__int128)a.q.den * b.q.den);
+/* OFAdd, numOprts.c:19-26 */
+static int of_add(int64_t a, int64_t b) {
+    return (a > 0 && b > INT64_MAX - a) || (a < 0 && b < INT64_MIN - a);
 }
+
+/* FractionAdd, numOprts.c:77-129 (NAdd of two numbers without a constant,
+ * numOprts.c:137-196: the main part's validity is the result's) */
+static Num add(Ctx *c, Num a, Num b) {
+    Num r = {{0, 0}, 1};
+    const int64_t pn = a.q.num, pd = a.q.den, nn = b.q.num, nd = b.q.den;
+    if (pd == 0 || nd == 0) {
+        r.valid = 0;
+        return r;
+    }
+    const int64_t cm = ref_lcm(c, pd, nd);
+    if (cm == -1) r.valid = 0;
+    const int64_t pf = c_div(c, cm, pd), pa = w_mul(pn, pf);
+    const int64_t nf = c_div(c, cm, nd), na = w_mul(nn, nf);
+    if ((pn != 0 && c_div(c, pa, pn) != pf) || (nn != 0 && c_div(c, na, nn) != nf)) r.valid = 0;
+    if (of_add(pa, na)) {
+        r.valid = 0;   /* numerator and denominator stay 0 */
+    } else {
+        int64_t s = pa + na, den = cm;
+        const int64_t g = ref_gcd(c, s, den);
+        s = c_div(c, s, g);
+        den = c_div(c, den, g);
+        r.q.num = s;
+        r.q.den = den;
+    }
+    return r;
+}
+
+/* NInv, numOprts.c:290-294: no check, LONG_MIN stays LONG_MIN */
 static Num neg(Num a) {
-    a.q.num = -a.q.num;
+    a.q.num = w_neg(a.q.num);
     return a;
 }
-static double dec(Num a) { return a.valid ? (double)a.q.num / (double)a.q.den : 0.0; }   /* Decimalize */
 
-/* C strtol over the whole string: 1 if fully consumed */
+/* NMul(Fractionize("-1"), a): FractionMul(-1, 1, n, d), numOprts.c:37-66 (the
+ * free-variable split, simplex.c:131, 154): -1 x LONG_MIN's check divides
+ * LONG_MIN by -1, which traps */
+static Num mul_m1(Ctx *c, Num a) {
+    if (a.q.den == 0) return (Num){{0, 0}, 0};
+    const int64_t p = w_neg(a.q.num);
+    (void)c_div(c, p, -1);
+    return (Num){{p, a.q.den}, 1};
+}
+
+/* Decimalize, basicFuncs.c:298-313 */
+static double dec(Num a) { return (a.valid && a.q.den) ? (double)a.q.num / (double)a.q.den : 0.0; }
+
+/* The value handed on (the SimplexMatrix): sign on the numerator, reduced */
+static lpf_q canon(Ctx *c, Num a) {
+    if (!a.valid || a.q.den == 0) die(c, "ERROR: an invalid number reached the SimplexMatrix");
+    __int128 n = a.q.num, d = a.q.den;
+    if (d < 0) n = -n, d = -d;
+    __int128 x = n < 0 ? -n : n, y = d;
+    while (y) {
+        const __int128 t = x % y;
+        x = y;
+        y = t;
+    }
+    if (x > 1) n /= x, d /= x;
+    if (n >= ((__int128)1 << 63) || -n > ((__int128)1 << 63) || d >= ((__int128)1 << 63))
+        die(c, "ERROR: a value outside int64 reached the SimplexMatrix");
+    return (lpf_q){(int64_t)n, (int64_t)d};
+}
+
+/* (long) of a double as x86-64 converts it: out of range or NaN -> LONG_MIN */
+static int64_t d2l(double x) {
+    if (!(x >= -9223372036854775808.0 && x < 9223372036854775808.0)) return INT64_MIN;
+    return (int64_t)x;
+}
+
+/* strtol over the whole string (saturating, as the reference's strtol): 1 if fully consumed */
 static int full_strtol(const char *s, int64_t *v) {
     char *end;
     long long x = strtoll(s, &end, 10);
@@ -133,25 +221,27 @@ static Num fractionize(Ctx *c, const char *str) {
     if (strchr(s, '/')) {
         char *save = NULL, *t1 = strtok_r(s, "/", &save), *t2 = t1 ? strtok_r(NULL, "/", &save) : NULL;
         int64_t n, d;
-        if (!t1 || !t2 || !full_strtol(t1, &n) || !full_strtol(t2, &d) || n == 0) return bad;
-        int64_t g = gcd64(n, d);
-        n /= g;
-        d /= g;
-        if (d <= 0) return bad;
-        return (Num){{n, d}, 1};
+        if (!t1 || !full_strtol(t1, &n) || !t2 || !full_strtol(t2, &d) || n == 0) return bad;
+        const int64_t g = w_labs(ref_gcd(c, n, d));
+        d = c_div(c, d, g);
+        n = c_div(c, n, g);
+        return (Num){{n, d}, d > 0};   /* basicFuncs.c:219-220: a denominator <= 0 is invalid */
     }
     if (s[0] == '\0' || (s[1] == '\0' && (s[0] == '+' || s[0] == '-'))) strcat(s, "1");
     if (strchr(s, '.')) {
         char *end;
-        double v = strtod(s, &end);
+        const double v = strtod(s, &end);
         if (*end != '\0') return bad;
         char cp[256], *save = NULL;
         strcpy(cp, s);
         char *t1 = strtok_r(cp, ".", &save), *t2 = t1 ? strtok_r(NULL, ".", &save) : NULL;
         if (!t2) return bad;
-        const int64_t den = (int64_t)pow(10.0, (double)strlen(t2));
-        const int64_t num = (int64_t)(v * (double)den);   /* truncation, basicFuncs.c:264 */
-        return mk(c, num, den);
+        int64_t den = d2l(pow(10.0, (double)strlen(t2)));
+        int64_t num = d2l(v * (double)den);   /* truncation, basicFuncs.c:264 */
+        const int64_t g = w_labs(ref_gcd(c, num, den));
+        den = c_div(c, den, g);
+        num = c_div(c, num, g);
+        return (Num){{num, den}, 1};          /* no denominator check on this path (basicFuncs.c:262-270) */
     }
     int64_t v;
     if (!full_strtol(s, &v)) return bad;
@@ -300,20 +390,23 @@ static Formula parse_formula(Ctx *c, const char *s) {
         }
     }
     if (f.l.n < 1 || f.r.n < 1 || !f.rel) die(c, "Simplification Failed: Formula invalid.");
-    int64_t gn = -1, gd = -1;
+    /* FormulaSimplify (dataReader.c:395-432): the common divisors of every
+     * numerator and every denominator, valid or not, start from the first
+     * term's own values; each is divided in place (C division, no reduction) */
+    int64_t gn = f.l.t[0].c.q.num, gd = f.l.t[0].c.q.den;
+    for (int side2 = 0; side2 < 2; side2++) {
+        Terms *v = side2 ? &f.r : &f.l;
+        for (int64_t k = side2 ? 0 : 1; k < v->n; k++) {
+            gn = ref_gcd(c, gn, v->t[k].c.q.num);
+            gd = ref_gcd(c, gd, v->t[k].c.q.den);
+        }
+    }
     for (int side2 = 0; side2 < 2; side2++) {
         Terms *v = side2 ? &f.r : &f.l;
         for (int64_t k = 0; k < v->n; k++) {
-            const int64_t a = v->t[k].c.valid ? v->t[k].c.q.num : 0, b = v->t[k].c.valid ? v->t[k].c.q.den : 0;
-            gn = gn < 0 ? (a < 0 ? -a : a) : gcd64(gn, a);
-            gd = gd < 0 ? (b < 0 ? -b : b) : gcd64(gd, b);
+            v->t[k].c.q.num = c_div(c, v->t[k].c.q.num, gn);
+            v->t[k].c.q.den = c_div(c, v->t[k].c.q.den, gd);
         }
-    }
-    if (gn == 0 || gd == 0) die(c, "Simplification Failed: division by a zero common divisor");
-    for (int side2 = 0; side2 < 2; side2++) {
-        Terms *v = side2 ? &f.r : &f.l;
-        for (int64_t k = 0; k < v->n; k++)
-            if (v->t[k].c.valid) v->t[k].c = mk(c, v->t[k].c.q.num / gn, v->t[k].c.q.den / gd);
     }
     return f;
 }
@@ -410,13 +503,13 @@ static void lp_trans(Ctx *c, Model *m) {
         for (int64_t j = 0; j < st->l.n; j++)   /* j then skips the shifted term, as the reference */
             if (st->l.t[j].var[0] == '\0') {
                 Term t = t_del(&st->l, j);
-                if (t.c.valid) t.c = neg(t.c);
+                t.c = neg(t.c);
                 t_push(c, &st->r, t);
             }
         for (int64_t j = 0; j < st->r.n; j++)
             if (st->r.t[j].var[0] != '\0') {
                 Term t = t_del(&st->r, j);
-                if (t.c.valid) t.c = neg(t.c);
+                t.c = neg(t.c);
                 t_push(c, &st->l, t);
             }
         if (st->l.n <= 0 || st->r.n <= 0)
@@ -498,7 +591,7 @@ static void standardize(Ctx *c, Model *m) {
             former.c = oc;
             m->obj.t[i] = former;
             Term latter = slack(c, m, &sub);
-            latter.c = neg(oc);
+            latter.c = mul_m1(c, oc);
             t_insert(c, &m->obj, i + 1, latter);
             it = t_get(&m->tb, target);   /* the table may have grown */
             snprintf(it->former, sizeof it->former, "%s", former.var);
@@ -511,7 +604,7 @@ static void standardize(Ctx *c, Model *m) {
                         const Num ck = l->t[k].c;
                         Term a = former, b = latter;
                         a.c = ck;
-                        b.c = neg(ck);
+                        b.c = mul_m1(c, ck);
                         l->t[k] = a;
                         t_insert(c, l, k + 1, b);
                         k++;
@@ -582,10 +675,10 @@ int lpf_build(const char *text, lpf_smatrix *out, char *err, size_t errlen) {
     align(&c, &m);
     /* CreateSMatrix (matrix.c:19-91): the constant dropped, the identity heuristic, the lack list */
     int64_t n = 0;
-    Num constant = {{0, 1}, 1};
+    Num constant = {{0, 1}, 1};   /* after CmbSmlTerms: at most one constant term */
     for (int64_t j = 0; j < m.obj.n; j++) {
         if (m.obj.t[j].var[0]) n++;
-        else constant = add(&c, constant, m.obj.t[j].c);
+        else constant = m.obj.t[j].c;
     }
     out->m = m.nrows;
     out->n = n;
@@ -601,27 +694,28 @@ int lpf_build(const char *text, lpf_smatrix *out, char *err, size_t errlen) {
         if (!m.obj.t[q].var[0]) continue;
         snprintf(out->names[j], 24, "%s", m.obj.t[q].var);
         out->inverted[j] = (unsigned char)m.obj.t[q].inv;
-        out->costs[j] = m.obj.t[q].c.q;
+        out->costs[j] = canon(&c, m.obj.t[q].c);
         j++;
     }
     for (int64_t i = 0; i < m.nrows; i++) {
         if (m.rows[i].l.n < n) die(&c, "ERROR occurred during the Standardization and the Alignment :( ");
-        out->rows[i * (n + 1)] = m.rows[i].r.t[0].c.q;
-        for (j = 0; j < n; j++) out->rows[i * (n + 1) + j + 1] = m.rows[i].l.t[j].c.q;
+        out->rows[i * (n + 1)] = canon(&c, m.rows[i].r.t[0].c);
+        for (j = 0; j < n; j++) out->rows[i * (n + 1) + j + 1] = canon(&c, m.rows[i].l.t[j].c);
     }
     for (j = 0; j < n; j++) {
         int ident = 0;
         int64_t pos = 0;
         for (int64_t i = 0; i < m.nrows; i++) {
-            const lpf_q v = out->rows[i * (n + 1) + j + 1];
-            const double d = (double)v.num / (double)v.den;
+            const double d = dec(m.rows[i].l.t[j].c);
             if (d == 1.0) pos = i;
-            ident += d >= 0 ? (int)d : 6;
+            /* int identityPart += (int) decimalized (x86-64: out of range -> INT_MIN), wrapping */
+            const int32_t di = (d >= -2147483648.0 && d < 2147483648.0) ? (int32_t)d : INT32_MIN;
+            ident = (int)(int32_t)((uint32_t)ident + (uint32_t)(d >= 0 ? di : 6));
         }
         if (ident == 1) out->basis[pos] = j + 1;
     }
-    out->constant = constant.q;
-    out->zcoef = m.zcoef.q;
+    out->constant = canon(&c, constant);
+    out->zcoef = canon(&c, m.zcoef);
     out->nvars = m.tb.n;
     memcpy(out->vars, m.tb.v, (size_t)m.tb.n * sizeof(lpf_var));
     for (int64_t q = 1; q < out->nvars; q++) {   /* GetVarItems order: stable by bucket (insertion order within) */

@@ -23,8 +23,11 @@ the reference binary's transcripts). Stages, each citing what it restates:
 
 The variable table mirrors hashTable.c (PutVarItem replaces an existing key in
 place; GetVarItems walks buckets in hash order, VarHash hashTable.c:148-167).
-Numbers are exact rationals (numOprts.c); the reference's ``long`` overflow
-checks are approximated by refusing any numerator / denominator outside int64.
+Numbers follow the reference's ``long`` arithmetic step for step (RNum:
+Fractionize, FractionAdd / NAdd, NInv, GCD / LCM with their wrap-around
+overflow checks, numOprts.c / basicFuncs.c), so exactly the models whose
+arithmetic the reference rejects are rejected; the SimplexMatrix is then
+handed on as exact rationals.
 The symbolic constant M is refused: user input may not carry it
 (dataReader.c:413-417).
 
@@ -47,10 +50,126 @@ class FrontendError(ValueError):
     """The reference would mark the model invalid (or crash) here."""
 
 
-def _chk(x: Fraction) -> Fraction:
-    if abs(x.numerator) >= _I64 or x.denominator >= _I64:
-        raise FrontendError(f"WARNING: operation overflowed ({x})")
-    return x
+# ---- the reference's `long` arithmetic, operation for operation -------------
+# Every coefficient of the reference is a pair of C longs, and its sums and
+# products are guarded by checks that rely on wrap-around (numOprts.c:19-26,
+# 37-129; basicFuncs.c:123-158; the reference is built -O0 -fwrapv). RNum
+# redoes each step with explicit 64-bit wrap, so a value the reference's
+# checks reject (an intermediate that wraps, though the reduced result would
+# fit) is rejected here too, and an invalid value keeps the numerator and
+# denominator the reference keeps (a later sum may use them). Where the
+# reference's own arithmetic traps (x / 0, LONG_MIN / -1: SIGFPE on x86-64)
+# the model is refused instead (tests/test_frontend.py records these).
+# host/lpfront.c carries the same restatement in C.
+_I64MIN, _I64MAX = -_I64, _I64 - 1
+
+
+def _w64(x: int) -> int:
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >= _I64 else x
+
+
+def _cdiv(a: int, b: int) -> int:
+    """C division (truncating); the trapping cases of x86-64 idiv refuse the model."""
+    if b == 0 or (a == _I64MIN and b == -1):
+        raise FrontendError("ERROR: arithmetic trap (the reference dies with SIGFPE here)")
+    q = abs(a) // abs(b)
+    return q if (a < 0) == (b < 0) else -q
+
+
+def _cmod(a: int, b: int) -> int:
+    return a - b * _cdiv(a, b)
+
+
+def _labs(a: int) -> int:
+    return _w64(-a) if a < 0 else a               # labs(LONG_MIN) == LONG_MIN
+
+
+def _rgcd(a: int, b: int) -> int:
+    """GCD, basicFuncs.c:123-137."""
+    a, b = _labs(a), _labs(b)
+    if b > a:
+        a, b = b, a
+    while b:
+        a, b = b, _cmod(a, b)
+    return a
+
+
+def _rlcm(a: int, b: int) -> int:
+    """LCM, basicFuncs.c:145-158: -1 when the product wraps."""
+    d = _rgcd(a, b)
+    a, b = _labs(a), _labs(b)
+    q = _cdiv(a, d)
+    r = _w64(q * b)
+    if q != 0 and _cdiv(r, q) != b:
+        return -1
+    return r
+
+
+def _d2l(x: float) -> int:
+    """(long) of a double as x86-64 converts it: out of range or NaN -> LONG_MIN."""
+    if not (-9223372036854775808.0 <= x < 9223372036854775808.0):
+        return _I64MIN
+    return int(x)
+
+
+def _w32(x: int) -> int:
+    x &= (1 << 32) - 1
+    return x - (1 << 32) if x >= 1 << 31 else x
+
+
+def _d2i(x: float) -> int:
+    """(int) of a double as x86-64 converts it: out of range or NaN -> INT_MIN."""
+    if not (-2147483648.0 <= x < 2147483648.0):
+        return -(1 << 31)
+    return int(x)
+
+
+class RNum:
+    """A reference Number without a constant: (numerator, denominator, valid)."""
+    __slots__ = ("num", "den", "valid")
+
+    def __init__(self, num: int, den: int, valid: bool = True):
+        self.num, self.den, self.valid = num, den, valid
+
+    def __neg__(self):                            # NInv, numOprts.c:290-294: no check
+        return RNum(_w64(-self.num), self.den, self.valid)
+
+    def __add__(self, o):                         # NAdd -> FractionAdd, numOprts.c:77-196
+        pn, pd, nn, nd = self.num, self.den, o.num, o.den
+        if pd == 0 or nd == 0:
+            return RNum(0, 0, False)
+        valid = True
+        cm = _rlcm(pd, nd)
+        if cm == -1:
+            valid = False
+        pf = _cdiv(cm, pd)
+        pa = _w64(pn * pf)
+        nf = _cdiv(cm, nd)
+        na = _w64(nn * nf)
+        if (pn != 0 and _cdiv(pa, pn) != pf) or (nn != 0 and _cdiv(na, nn) != nf):
+            valid = False
+        if (pa > 0 and na > _I64MAX - pa) or (pa < 0 and na < _I64MIN - pa):   # OFAdd
+            return RNum(0, 0, False)
+        s, den = pa + na, cm
+        g = _rgcd(s, den)
+        return RNum(_cdiv(s, g), _cdiv(den, g), valid)
+
+    def mul_m1(self):
+        """NMul(Fractionize("-1"), x) = FractionMul(-1, 1, n, d) (numOprts.c:37-66; the
+        free-variable split, simplex.c:131, 154): its check divides -n by -1, which
+        traps for n = LONG_MIN."""
+        if self.den == 0:
+            return RNum(0, 0, False)
+        p = _w64(-self.num)
+        _cdiv(p, -1)
+        return RNum(p, self.den)
+
+    def value(self) -> Fraction:
+        return Fraction(self.num, self.den)
+
+    def __repr__(self):
+        return f"RNum({self.num}/{self.den}{'' if self.valid else ' invalid'})"
 
 
 def _strtol(s: str):
@@ -74,48 +193,54 @@ def _tokens(s: str, d: str):
     return [t for t in s.split(d) if t]          # strtok: empty tokens skipped
 
 
-def fractionize(s: str):
-    """Fractionize (basicFuncs.c:165-291) without constants: Fraction or None (invalid)."""
+def fractionize(s: str) -> RNum:
+    """Fractionize (basicFuncs.c:165-291) without constants."""
+    bad = RNum(0, 0, False)
     if "M" in s:
         raise FrontendError("Simplification Failed: Manual added CONSTANTs are not allowed.")
     if "/" in s:
         tk = _tokens(s, "/")
-        if len(tk) < 2:
-            return None
+        if not tk:
+            return bad
         num, ok = _strtol(tk[0])
+        if not ok or len(tk) < 2:
+            return bad
         den, ok2 = _strtol(tk[1])
-        if not ok or not ok2 or num == 0:
-            return None
-        g = gcd(num, den)                         # >= 1: num != 0
-        num, den = num // g, den // g
-        if den <= 0:
-            return None
-        return Fraction(num, den)
+        if not ok2 or num == 0:
+            return bad
+        g = _labs(_rgcd(num, den))
+        den = _cdiv(den, g)
+        num = _cdiv(num, g)
+        return RNum(num, den, den > 0)            # basicFuncs.c:219-220: a denominator <= 0 is invalid
     if s == "" or s in ("+", "-"):
         s = s + "1"
     if "." in s:
         try:
             dec = float(s)
         except ValueError:
-            return None
+            return bad
         tk = _tokens(s, ".")
         if len(tk) < 2:
-            return None
-        den = int(10.0 ** len(tk[1]))
-        num = int(dec * float(den))               # (long)(decimal * denominator): truncation (basicFuncs.c:264)
-        return Fraction(num, den)
+            return bad
+        den = _d2l(10.0 ** len(tk[1]))
+        num = _d2l(dec * float(den))              # (long)(decimal * denominator): truncation (basicFuncs.c:264)
+        g = _labs(_rgcd(num, den))
+        return RNum(_cdiv(num, g), _cdiv(den, g))  # no denominator check on this path (basicFuncs.c:262-270)
     v, ok = _strtol(s)
-    return Fraction(v) if ok else None
+    return RNum(v, 1) if ok else bad
 
 
 def _dec(x) -> float:
-    """Decimalize (basicFuncs.c:298-313): (double) n / d; 0 for an invalid number."""
-    return 0.0 if x is None else float(x.numerator) / float(x.denominator)
+    """Decimalize (basicFuncs.c:298-313): (double) n / d; 0 for an invalid number or d = 0.
+    Takes an RNum, or a Fraction of the SimplexMatrix handed on."""
+    if isinstance(x, Fraction):
+        return float(x.numerator) / float(x.denominator)
+    return float(x.num) / float(x.den) if (x is not None and x.valid and x.den) else 0.0
 
 
 @dataclass
 class Term:
-    coef: object                 # Fraction, or None where the reference's Number is invalid
+    coef: object                 # RNum (the reference's Number, valid or not)
     var: str = ""
     inverted: bool = False
 
@@ -197,9 +322,9 @@ def _formula(s: str) -> Formula:
     while i < n + 1:
         ch = s[i] if i < n else "+"
         if ch in "+->=<":
-            if buf or coef is not None:
-                t = Term(coef)
-                if not buf and coef is not None:
+            if buf or (coef is not None and coef.valid):
+                t = Term(coef if coef is not None else RNum(0, 0, False))
+                if not buf and coef is not None and coef.valid:
                     t.var = ""
                 elif all(c in "0123456789/+-.M" for c in buf):   # IsConstTerm
                     t.coef, t.var = fractionize(buf), ""
@@ -222,23 +347,21 @@ def _formula(s: str) -> Formula:
                 f.relation, side = 3, 1
         else:
             if not cfc and ch not in "0123456789./":
-                coef = fractionize(buf) if buf else Fraction(1)
+                coef = fractionize(buf) if buf else RNum(1, 1)
                 buf, cfc = "", True
             buf += ch
         i += 1
     if not f.left or not f.right or not f.relation:
         raise FrontendError("Simplification Failed: Formula invalid.")
+    # FormulaSimplify: the common divisors of every numerator and every
+    # denominator, valid or not, from the first term's own values; each one
+    # divided in place (C division, no reduction)
     joined = f.left + f.right
-    nums = [0 if t.coef is None else t.coef.numerator for t in joined]
-    dens = [0 if t.coef is None else t.coef.denominator for t in joined]
-    gn, gd = abs(nums[0]), abs(dens[0])
-    for a, b in zip(nums[1:], dens[1:]):
-        gn, gd = gcd(gn, a), gcd(gd, b)
-    if gn == 0 or gd == 0:
-        raise FrontendError("Simplification Failed: division by a zero common divisor")
+    gn, gd = joined[0].coef.num, joined[0].coef.den
+    for t in joined[1:]:
+        gn, gd = _rgcd(gn, t.coef.num), _rgcd(gd, t.coef.den)
     for t in joined:
-        if t.coef is not None:
-            t.coef = Fraction(t.coef.numerator // gn, t.coef.denominator // gd)   # exact: gn, gd divide them
+        t.coef = RNum(_cdiv(t.coef.num, gn), _cdiv(t.coef.den, gd), t.coef.valid)
     return f
 
 
@@ -301,14 +424,13 @@ def _combine(terms: list, table: VarTable, record: bool) -> None:
         k = j + 1
         while k < len(terms):
             if terms[j].var == terms[k].var:
-                a, b = terms[j].coef, terms[k].coef
-                terms[j].coef = None if a is None or b is None else _chk(a + b)
+                terms[j].coef = terms[j].coef + terms[k].coef
                 del terms[k]
                 k -= 1
             k += 1
-        if terms[j].coef is None:
+        if not terms[j].coef.valid:
             raise FrontendError("CMB ERROR: Invalid coefficient appeared after combining.")
-        if terms[j].coef.numerator == 0:
+        if terms[j].coef.num == 0:
             del terms[j]
             j -= 1
         elif record:
@@ -327,27 +449,26 @@ def lp_trans(m: Model) -> Model:
         while j < len(st.left):                    # j advances past the shifted term (the reference's loop)
             if st.left[j].var == "":
                 t = st.left.pop(j)
-                t.coef = None if t.coef is None else -t.coef
+                t.coef = -t.coef
                 st.right.append(t)
             j += 1
         j = 0
         while j < len(st.right):
             if st.right[j].var != "":
                 t = st.right.pop(j)
-                t.coef = None if t.coef is None else -t.coef
+                t.coef = -t.coef
                 st.left.append(t)
             j += 1
         if not st.left or not st.right:
             raise FrontendError(f"ERROR: LPModel invalid due to the incomplete CONSTRAINT (ST Line: {i + 1}).")
         _combine(st.left, m.vars, record=True)
         for j in range(len(st.right) - 1, 0, -1):
-            a, b = st.right[0].coef, st.right[j].coef
-            st.right[0].coef = None if a is None or b is None else _chk(a + b)
+            st.right[0].coef = st.right[0].coef + st.right[j].coef
             del st.right[j]
         if not st.left:
             raise FrontendError(f"ERROR: No term left in the left hand side of the CONSTRAINT (ST Line: {i + 1}) "
                                 "after combining similar terms.")
-        if st.right[0].coef is None:
+        if not st.right[0].coef.valid:
             raise FrontendError(f"ERROR: Division by zero appeared in the right hand side of the CONSTRAINT "
                                 f"(ST Line: {i + 1}).")
         if (len(st.left) == 1 and len(st.right) == 1 and _dec(st.left[0].coef) == 1
@@ -404,7 +525,7 @@ def standardize(m: Model, dual: bool = False) -> Model:
         sub[0] += 1
         name = f"x{sub[0]}"
         m.vars.put(VarItem(name, 2))
-        return Term(Fraction(0), name)
+        return Term(RNum(0, 1), name)
 
     if m.otype != 1:
         m.otype = 1
@@ -421,7 +542,7 @@ def standardize(m: Model, dual: bool = False) -> Model:
             former.coef = c
             m.objective[i] = former
             latter = slack()
-            latter.coef = -c
+            latter.coef = c.mul_m1()
             m.objective.insert(i + 1, latter)
             it.former, it.latter = former.var, latter.var
             i += 1
@@ -431,7 +552,7 @@ def standardize(m: Model, dual: bool = False) -> Model:
                     if st.left[k].var == target:
                         ck = st.left[k].coef
                         st.left[k] = Term(ck, former.var, former.inverted)
-                        st.left.insert(k + 1, Term(-ck, latter.var, latter.inverted))
+                        st.left.insert(k + 1, Term(ck.mul_m1(), latter.var, latter.inverted))
                         k += 1
                     k += 1
         i += 1
@@ -447,7 +568,7 @@ def standardize(m: Model, dual: bool = False) -> Model:
             s = slack()
             m.objective.append(s)
             s = s.copy()
-            s.coef = Fraction(-1) if st.relation > 0 else Fraction(1)
+            s.coef = RNum(-1, 1) if st.relation > 0 else RNum(1, 1)
             st.relation = 3
             st.left.append(s)
         _sort(st.left)
@@ -465,7 +586,7 @@ def align(m: Model) -> Model:
             if t.var:
                 if k >= len(st.left) or st.left[k].var != t.var:
                     z = t.copy()
-                    z.coef = Fraction(0)
+                    z.coef = RNum(0, 1)
                     st.left.insert(k, z)
                 k += 1
     return m
@@ -491,7 +612,7 @@ class SMatrix:
 
 def smatrix(m: Model) -> SMatrix:
     """CreateSMatrix (matrix.c:19-91), the lack list written correctly."""
-    constant = sum((t.coef for t in m.objective if not t.var), Fraction(0))
+    constant = sum((t.coef.value() for t in m.objective if not t.var), Fraction(0))
     of = [t for t in m.objective if t.var]
     rows = []
     for st in m.rows:
@@ -505,11 +626,12 @@ def smatrix(m: Model) -> SMatrix:
             d = _dec(r[j + 1])
             if d == 1:
                 pos = i
-            ident += int(d) if d >= 0 else 6
+            ident = _w32(ident + (_d2i(d) if d >= 0 else 6))   # int identityPart, (int) decimalized
         if ident == 1:
             basis[pos] = j + 1
-    return SMatrix([t.var for t in of], [t.inverted for t in of], [t.coef for t in of], rows, basis,
-                   [i for i, b in enumerate(basis) if b == 0], constant, m.zcoef, m.vars)
+    rows = [[x.value() for x in r] for r in rows]
+    return SMatrix([t.var for t in of], [t.inverted for t in of], [t.coef.value() for t in of], rows, basis,
+                   [i for i, b in enumerate(basis) if b == 0], constant, m.zcoef.value(), m.vars)
 
 
 def build_smatrix(text: str, dual: bool = False) -> SMatrix:

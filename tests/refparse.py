@@ -15,12 +15,11 @@ the reference's quirk that accepts a non-unit column such as (3/2, 1/2).
 """
 from __future__ import annotations
 
-import math
 import re
 from dataclasses import dataclass, field
 from fractions import Fraction
 
-_TERM = re.compile(r"(-?\d+)(M?)(?:/(\d+)(M?))?(?:\[([^\]]*)\])?")
+_TERM = re.compile(r"(-?\d+)(M?)(?:/(-?\d+)(M?))?(?:\[([^\]]*)\])?")
 
 
 def parse_terms(s: str):
@@ -36,7 +35,10 @@ def parse_terms(s: str):
         num, m1, den, m2, var = mt.groups()
         if m1 or m2:
             raise ValueError("Big-M coefficients are not representable as fp64")
-        val = Fraction(int(num), int(den) if den else 1) * sign
+        # PrintTerms prints a later term as " - labs(n)", and labs(LONG_MIN) is
+        # LONG_MIN: " - -9223372036854775808" means the numerator LONG_MIN itself
+        n = int(num)
+        val = Fraction(n if (sign < 0 and n < 0) else n * sign, int(den) if den else 1)
         var = var or ""
         inverted = var.endswith("'")
         out.append((val, var.rstrip("'"), inverted))
@@ -124,9 +126,11 @@ def tableau_from_aligned(model: PrintedModel) -> RefTableau:
         pos = 0
         for i in range(m):
             x = T[i][j + 1]
-            if x == 1:
+            d = float(x.numerator) / float(x.denominator)       # Decimalize
+            if d == 1.0:
                 pos = i
-            ident += math.floor(x) if x >= 0 else 6
+            di = int(d) if -2147483648.0 <= d < 2147483648.0 else -(1 << 31)   # (int) d on x86-64
+            ident = ((ident + (di if d >= 0 else 6) + (1 << 31)) % (1 << 32)) - (1 << 31)   # int, wrapping
         if ident == 1:
             basis[pos] = j + 1
     lacking = [i for i in range(m) if basis[i] == 0]

@@ -67,13 +67,13 @@ def test_shipped_testdata_is_rejected_like_the_reference():
 def test_decimal_truncation_and_gcd_quirks():
     """Fractionize's (long)(d * 10^k) truncation (basicFuncs.c:264) and
     FormulaSimplify's separate numerator / denominator GCDs (dataReader.c:409-428)."""
-    assert F.fractionize("0.29") == Fraction(28, 100)          # 0.29 * 100 = 28.999...
-    assert F.fractionize("-2.45") == Fraction(-49, 20)
-    assert F.fractionize("0/5") is None and F.fractionize(".5") is None
+    assert F.fractionize("0.29").value() == Fraction(28, 100)  # 0.29 * 100 = 28.999...
+    assert F.fractionize("-2.45").value() == Fraction(-49, 20)
+    assert not F.fractionize("0/5").valid and not F.fractionize(".5").valid
     f = F._formula("2x1+4x2<=6")
-    assert [t.coef for t in f.left] == [1, 2] and f.right[0].coef == 3
+    assert [t.coef.value() for t in f.left] == [1, 2] and f.right[0].coef.value() == 3
     f = F._formula("1/2x1+1/4x2<=1/2")
-    assert [t.coef for t in f.left] == [1, Fraction(1, 2)] and f.right[0].coef == 1
+    assert [t.coef.value() for t in f.left] == [1, Fraction(1, 2)] and f.right[0].coef.value() == 1
 
 
 def test_sign_constraint_before_use_makes_the_variable_free():
@@ -254,10 +254,74 @@ def test_c_front_end_error_is_valid_json(tmp_path, bad):
     assert rc == 3 and got["error"].startswith("ERROR:")
 
 
+OVERFLOW = json.load(open(os.path.join(ROOT, "tests", "golden", "overflow_cases.json")))
+
+
+def _overflow_expectation(case, sm_or_error):
+    """Check one front end's result on one overflow fixture against the
+    reference binary's outcome (tests/golden/make_overflow_golden.py):
+    accepted -> the same aligned tableau; rejected, or SIGFPE (8: its
+    FormulaSimplify / NMul divide by 0 or LONG_MIN by -1) -> rejected here.
+    SIGSEGV (11) is the reference's CreateSMatrix writing `*lack[lackPtr++]`
+    (matrix.c:86; `*(lack[k])`, a wild stack pointer once k >= 1): it dies on
+    models with two or more rows lacking a unit column. The front ends keep the
+    intended lack list instead, so for those the check is that it has >= 2 rows."""
+    if case["outcome"] == "accepted":
+        assert not isinstance(sm_or_error, Exception), (case["name"], sm_or_error)
+        return
+    if case["outcome"] == "crash" and case["signal"] == 11:
+        assert not isinstance(sm_or_error, Exception), (case["name"], sm_or_error)
+        return
+    assert isinstance(sm_or_error, Exception), (case["name"], case["outcome"])
+
+
+@pytest.mark.parametrize("case", OVERFLOW, ids=lambda c: c["name"])
+def test_long_overflow_matches_the_reference(case):
+    """The reference's `long` arithmetic past its limits:
+    wrap-around guarded sums and products, LCM overflow, strtol saturation,
+    (long) casts of out-of-range doubles, NInv's unchecked LONG_MIN, traps."""
+    try:
+        sm = F.build_smatrix(case["text"])
+    except F.FrontendError as ex:
+        sm = ex
+    _overflow_expectation(case, sm)
+    if case["outcome"] == "crash" and case["signal"] == 11:
+        assert len(sm.lacking) >= 2
+    if case["outcome"] == "accepted":
+        ok, got, exp = _same(sm, case["names"], case["basis"], case["lacking"], [_fx(c) for c in case["costs"]],
+                             _fx(case["constant"]), _fx(case["zcoef"]), [[_fx(x) for x in r] for r in case["rows"]])
+        assert ok, (case["text"], got, exp)
+    elif case["outcome"] == "rejected" and "Invalid coefficient appeared after combining" in case["message"]:
+        assert "Invalid coefficient appeared after combining" in str(sm)
+
+
+@needs_cli
+def test_c_front_end_long_overflow_matches_the_reference(tmp_path):
+    """lpfront.c on the same overflow fixtures: accepted models dump the
+    reference's tableau; rejected and trapping ones exit 3 with an error line."""
+    for case in OVERFLOW:
+        f = tmp_path / "o.txt"
+        f.write_text(case["text"])
+        rc, got = _c_dump(str(f))
+        _overflow_expectation(case, RuntimeError(got["error"]) if rc == 3 else got)
+        assert rc in (0, 3), (case["name"], rc)
+        if case["outcome"] == "accepted":
+            exp = {k: case[k] for k in ("names", "basis", "costs", "constant", "zcoef", "rows")}
+            assert {k: got[k] for k in exp} == exp, (case["text"], got, exp)
+        if case["outcome"] == "crash" and case["signal"] == 8:
+            assert "arithmetic trap" in got["error"], (case["name"], got)
+
+
 @pytest.mark.skipif(not os.path.exists(SAN_CLI), reason="integration/_san/lpgcli not built")
 def test_c_front_end_under_asan_ubsan(tmp_path):
-    """The ASan + UBSan build of lpgcli on the fixtures and 40 random models, incl. rejected ones."""
+    """The ASan + UBSan build of lpgcli on the fixtures, the overflow fixtures
+    (its `long` emulation wraps in unsigned arithmetic: no UB on overflow) and
+    40 random models, incl. rejected ones."""
     files = [os.path.join(LP, f) for f in sorted(os.listdir(LP))]
+    for t, case in enumerate(OVERFLOW):
+        f = tmp_path / f"o{t}.txt"
+        f.write_text(case["text"])
+        files.append(str(f))
     rng = np.random.default_rng(7)
     for t in range(40):
         f = tmp_path / f"s{t}.txt"
