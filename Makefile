@@ -10,8 +10,8 @@ LIB       = linearprogramming_amd/liblpg.so
 
 all: $(LIB) host/lpgcli oracle
 
-$(LIB): $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h include/lpg.h
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_ctx.hip -ldl
+$(LIB): $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h include/lpg.h
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip -ldl
 
 host/lpgcli: host/lpgcli.c host/lpfront.c host/lpfront.h include/lpg.h $(LIB)
 	$(CC) -O2 -std=c11 -Wall -Wextra -Iinclude -o $@ host/lpgcli.c host/lpfront.c -L$(dir $(LIB)) -llpg -Wl,-rpath,'$$ORIGIN/../linearprogramming_amd' -lm
@@ -24,8 +24,8 @@ ref:
 
 # phase-stamped build for tools/phase_probe.py and tools/block_probe.py (diagnostics only)
 phases: tools/liblpg_phases.so
-tools/liblpg_phases.so: $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h
-	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_ctx.hip -ldl
+tools/liblpg_phases.so: $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h
+	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip -ldl
 
 asm: $(CSRC)/lpg_kernels.hip
 	$(HIPCC) $(HIPFLAGS) -c --save-temps -o /tmp/lpg_kernels.o $(CSRC)/lpg_kernels.hip

@@ -574,7 +574,12 @@ static Term slack(Ctx *c, Model *m, long long *sub) {   /* CreateSlack, simplex.
 }
 
 /* LPStandardize (simplex.c:91-230), primal form */
-static void standardize(Ctx *c, Model *m) {
+/* LPStandardize (simplex.c:91-230). dual = 0: rows with a negative right-hand
+ * side are negated; dual = 1 (simplex.c:178-179): every > / >= row is negated
+ * into < / <= instead, whatever the sign of b, so each inequality gets a +1
+ * slack (the dual simplex's starting basis; the reference's router never
+ * reaches this branch, router.c:32-34). */
+static void standardize(Ctx *c, Model *m, int dual) {
     long long sub = m->tb.max_x;
     if (m->otype != 1) {
         m->otype = 1;
@@ -614,7 +619,7 @@ static void standardize(Ctx *c, Model *m) {
     }
     for (int64_t r = 0; r < m->nrows; r++) {
         Formula *st = &m->rows[r];
-        if (dec(st->r.t[0].c) < 0) {
+        if ((!dual && dec(st->r.t[0].c) < 0) || (dual && st->rel > 0 && st->rel != 3)) {
             st->r.t[0].c = neg(st->r.t[0].c);
             for (int64_t k = 0; k < st->l.n; k++) st->l.t[k].c = neg(st->l.t[k].c);
             if (st->rel != 3) st->rel = -st->rel;
@@ -657,6 +662,10 @@ static int cmp_hash(const void *a, const void *b) {   /* GetVarItems order: buck
 }
 
 int lpf_build(const char *text, lpf_smatrix *out, char *err, size_t errlen) {
+    return lpf_build_form(text, 0, out, err, errlen);
+}
+
+int lpf_build_form(const char *text, int dual, lpf_smatrix *out, char *err, size_t errlen) {
     Ctx c;
     memset(&c, 0, sizeof c);
     c.err = err;
@@ -671,7 +680,7 @@ int lpf_build(const char *text, lpf_smatrix *out, char *err, size_t errlen) {
     memset(&m, 0, sizeof m);
     parse(&c, text, &m);
     lp_trans(&c, &m);
-    standardize(&c, &m);
+    standardize(&c, &m, dual);
     align(&c, &m);
     /* CreateSMatrix (matrix.c:19-91): the constant dropped, the identity heuristic, the lack list */
     int64_t n = 0;
@@ -746,8 +755,9 @@ void lpf_free(lpf_smatrix *sm) {
 
 static double qd(lpf_q q) { return (double)q.num / (double)q.den; }
 
-int lpf_solve(const lpf_smatrix *sm, int bigm, int rule, int device, lpf_solution *out, char *err, size_t errlen) {
+int lpf_solve(const lpf_smatrix *sm, int method, int rule, int device, lpf_solution *out, char *err, size_t errlen) {
     memset(out, 0, sizeof *out);
+    int bigm = method == LPF_BIG_M;
     const int64_t m = sm->m, nc0 = sm->n + 1;
     int64_t *basis = (int64_t *)calloc((size_t)(m ? m : 1), sizeof(int64_t));
     int64_t nlack = 0;
@@ -759,6 +769,17 @@ int lpf_solve(const lpf_smatrix *sm, int bigm, int rule, int device, lpf_solutio
                 if (v.num != (q == i ? 1 : 0) || (v.num != 0 && v.den != 1)) basis[i] = 0;
             }
         if (!basis[i]) nlack++;
+    }
+    if (method == LPF_DUAL) {   /* the slack basis must be complete and dual feasible (as frontend.py) */
+        const char *why = NULL;
+        if (nlack) why = "dual simplex: rows without a slack basis (equality rows); build the dual form";
+        for (int64_t j = 0; !why && j < sm->n; j++)
+            if (qd(sm->costs[j]) > 0) why = "dual simplex: the slack basis is not dual feasible (a positive max-form cost)";
+        if (why) {
+            if (err && errlen) snprintf(err, errlen, "%s", why);
+            free(basis);
+            return -1;
+        }
     }
     const int64_t nc = nc0 + nlack;
     double *rows = (double *)calloc((size_t)(m * nc), sizeof(double));
@@ -781,7 +802,9 @@ int lpf_solve(const lpf_smatrix *sm, int bigm, int rule, int device, lpf_solutio
     if (lpg_create(&ctx, device, m, nc, bigm ? LPG_FLAG_BIG_M : 0) || lpg_load_rows(ctx, 0, m, rows, nc) ||
         lpg_set_basis(ctx, basis))
         goto fail;
-    if (nlack == 0) {
+    if (method == LPF_DUAL) {
+        if (lpg_set_objective(ctx, cost) || lpg_solve_dual(ctx, (int64_t)1 << 40, &res)) goto fail;
+    } else if (nlack == 0) {
         if (lpg_set_objective(ctx, cost) || lpg_solve(ctx, (int64_t)1 << 40, rule, &res)) goto fail;
     } else if (bigm) {
         if (lpg_solve_big_m(ctx, nc0, cost, (int64_t)1 << 40, rule, &res)) goto fail;

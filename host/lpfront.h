@@ -45,6 +45,8 @@ typedef struct {
 
 /* 0 on success; otherwise -1 and the reference's message in err. */
 int lpf_build(const char *text, lpf_smatrix *out, char *err, size_t errlen);
+/* dual = 1: LPStandardize's dual form (simplex.c:178-179), for LPF_DUAL */
+int lpf_build_form(const char *text, int dual, lpf_smatrix *out, char *err, size_t errlen);
 void lpf_free(lpf_smatrix *sm);
 
 typedef struct {
@@ -56,8 +58,11 @@ typedef struct {
 } lpf_solution;
 
 /* Device solve as the bridge does it: artificials for rows without a true unit
- * column, two-phase (bigm = 0) or Big-M (bigm = 1). 0 on success. */
-int lpf_solve(const lpf_smatrix *sm, int bigm, int rule, int device, lpf_solution *out, char *err, size_t errlen);
+ * column, two-phase (LPF_TWO_PHASE) or Big-M (LPF_BIG_M); LPF_DUAL: the dual
+ * simplex from the slack basis of a dual-form matrix (lpf_build_form(.., 1, ..)),
+ * which must be complete and dual feasible. 0 on success. */
+enum { LPF_TWO_PHASE = 0, LPF_BIG_M = 1, LPF_DUAL = 2 };
+int lpf_solve(const lpf_smatrix *sm, int method, int rule, int device, lpf_solution *out, char *err, size_t errlen);
 void lpf_solution_free(lpf_solution *s);
 
 #ifdef __cplusplus

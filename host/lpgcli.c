@@ -13,6 +13,11 @@
  *   lpgcli --lp MODEL [--big-m] [--rule ...]     the reference's model format,
  *          through the C front end (lpfront.c) onto the device
  *   lpgcli --lp-dump MODEL                       the SimplexMatrix as JSON (no device)
+ *   --dual  the dual simplex (router option 2, router.c:32-34, which the
+ *          reference leaves empty): with --lp, LPStandardize's dual form
+ *          (simplex.c:178-179) solved from its slack basis; with --synthetic,
+ *          the dual-feasible LPG_GEN_DUAL tableau; with --tableau, the file's
+ *          (dual-feasible) basis. Single rank.
  *   lpgcli --synthetic M N --gpus P [--exchange push|host]
  *          the row partition over P ranks, one process each (forked before
  *          any HIP call; the parent only relays the host-staged collectives
@@ -53,7 +58,8 @@ static int usage(const char *argv0) {
     fprintf(stderr, "Usage:\n\t%s --synthetic M N [--seed S] [--kind dense|degenerate] [--rule dantzig|bland]"
                     " [--pivots K] [--device D] [--gpus P [--exchange push|host]]\n"
                     "\t%s --tableau FILE [--rule dantzig|bland] [--pivots K]\n"
-                    "\t%s --lp MODEL [--big-m] [--rule dantzig|bland]\n\t%s --lp-dump MODEL\n",
+                    "\t%s --lp MODEL [--big-m | --dual] [--rule dantzig|bland]\n\t%s --lp-dump MODEL [--dual]\n"
+                    "\t(--dual: the dual simplex; also with --synthetic and --tableau, single rank)\n",
             argv0, argv0, argv0, argv0);
     return 2;
 }
@@ -313,12 +319,12 @@ static void print_error(const char *err) {
 static void print_q(lpf_q q) { printf("\"%lld/%lld\"", (long long)q.num, (long long)q.den); }
 
 /* the reference model file -> SimplexMatrix (dump) or the device optimum */
-static int run_lp(const char *path, int dump, int bigm, int rule, int device) {
+static int run_lp(const char *path, int dump, int method, int rule, int device) {
     char err[512] = "";
     char *text = read_all(path);
     if (!text) return 1;
     lpf_smatrix sm;
-    const int rc = lpf_build(text, &sm, err, sizeof err);
+    const int rc = lpf_build_form(text, method == LPF_DUAL, &sm, err, sizeof err);
     free(text);
     if (rc) {
         print_error(err);
@@ -367,7 +373,7 @@ static int run_lp(const char *path, int dump, int bigm, int rule, int device) {
         return 0;
     }
     lpf_solution sol;
-    if (lpf_solve(&sm, bigm, rule, device, &sol, err, sizeof err)) {
+    if (lpf_solve(&sm, method, rule, device, &sol, err, sizeof err)) {
         print_error(err);
         lpf_free(&sm);
         return 1;
@@ -428,7 +434,7 @@ int main(int argc, char **argv) {
     unsigned long long seed = 20220518ull;
     int kind = LPG_GEN_DENSE, rule = LPG_RULE_DANTZIG, device = 0, gpus = 1, push = 1;
     const char *file = NULL, *lpfile = NULL;
-    int dump = 0, bigm = 0;
+    int dump = 0, bigm = 0, dual = 0;
     for (int a = 1; a < argc; a++) {
         if (!strcmp(argv[a], "--synthetic") && a + 2 < argc) {
             m = atoll(argv[++a]);
@@ -440,6 +446,8 @@ int main(int argc, char **argv) {
             lpfile = argv[++a];
         } else if (!strcmp(argv[a], "--big-m")) {
             bigm = 1;
+        } else if (!strcmp(argv[a], "--dual")) {
+            dual = 1;
         } else if (!strcmp(argv[a], "--seed") && a + 1 < argc) {
             seed = strtoull(argv[++a], NULL, 10);
         } else if (!strcmp(argv[a], "--kind") && a + 1 < argc) {
@@ -458,7 +466,8 @@ int main(int argc, char **argv) {
             return usage(argv[0]);
         }
     }
-    if (lpfile) return run_lp(lpfile, dump, bigm, rule, device);
+    if (dual && (bigm || gpus > 1)) return usage(argv[0]);
+    if (lpfile) return run_lp(lpfile, dump, dual ? LPF_DUAL : bigm ? LPF_BIG_M : LPF_TWO_PHASE, rule, device);
     if (gpus > 1) {
         if (!(m > 0 && n > 0) || gpus > m || gpus > 64) return usage(argv[0]);
         const dist_args da = {m, n, pivots, seed, kind, rule, device, gpus, push};
@@ -472,7 +481,8 @@ int main(int argc, char **argv) {
             return 1;
         }
     } else if (m > 0 && n > 0) {
-        if ((rc = lpg_create(&ctx, device, m, n + m + 1, 0)) != 0 || (rc = lpg_generate(ctx, n, seed, kind)) != 0) {
+        if ((rc = lpg_create(&ctx, device, m, n + m + 1, 0)) != 0 ||
+            (rc = lpg_generate(ctx, n, seed, dual ? LPG_GEN_DUAL : kind)) != 0) {
             fprintf(stderr, "ERROR: %s\n", lpg_last_error(ctx));
             lpg_destroy(ctx);
             return 1;
@@ -482,7 +492,7 @@ int main(int argc, char **argv) {
     }
     lpg_result res;
     const double t0 = now();
-    rc = lpg_solve(ctx, pivots, rule, &res);
+    rc = dual ? lpg_solve_dual(ctx, pivots, &res) : lpg_solve(ctx, pivots, rule, &res);
     const double dt = now() - t0;
     if (rc != 0) {
         fprintf(stderr, "ERROR: %s\n", lpg_last_error(ctx));
@@ -493,10 +503,10 @@ int main(int argc, char **argv) {
     lpg_info(ctx, &info);
     printf("{\"status\": \"%s\", \"pivots\": %lld, \"objective\": %.17g, \"seconds\": %.6f, "
            "\"pivots_per_s\": %.3f, \"m\": %lld, \"ncols\": %lld, \"rule\": \"%s\", \"gpus\": 1, "
-           "\"defer_k\": %d, \"log_fnv\": \"%016llx\"}\n",
+           "\"defer_k\": %d, \"method\": \"%s\", \"log_fnv\": \"%016llx\"}\n",
            status_name(res.status), (long long)res.pivots, res.objective, dt, dt > 0 ? (double)res.pivots / dt : 0.0,
-           (long long)info.m, (long long)info.ncols, rule == LPG_RULE_BLAND ? "bland" : "dantzig", info.defer_k,
-           (unsigned long long)log_fnv(ctx, res.pivots));
+           (long long)info.m, (long long)info.ncols, rule == LPG_RULE_BLAND && !dual ? "bland" : "dantzig", info.defer_k,
+           dual ? "dual" : "primal", (unsigned long long)log_fnv(ctx, res.pivots));
     lpg_destroy(ctx);
     return 0;
 }

@@ -54,6 +54,7 @@ struct lpg_ctx {
     int *pc = nullptr;            // npp live-slice counts of P (column-skipping accounting)
     Cand *part = nullptr;         // nsel (this rank's select partials)
     Cand *cand = nullptr;         // world * nsel (gathered); == part when world == 1
+    Cand *drc = nullptr, *dcp = nullptr;   // deferred dual: row candidates, ratio-test partials (lazy)
     int64_t *basis = nullptr;     // m (replicated)
     int64_t *logk = nullptr, *logr = nullptr;
     int64_t logcap = 0;
@@ -1110,7 +1111,7 @@ void lpg_destroy(lpg_ctx *c) {
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
                     c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->mul, c->pv, c->tmp,
-                    c->rec};
+                    c->rec, c->drc, c->dcp};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -1460,6 +1461,71 @@ int lpg_solve_big_m(lpg_ctx *c, int64_t art_first, const double *cost, int64_t m
     return 0;
 }
 
+// The dual on the deferred tableau (lpg_dual.hip): two kernels per pivot,
+// the block's flush (no column trade: the ratio test's keys are the caller's
+// column order) every defer_k pivots, and a final k_dual_row_d for the
+// objective row's owed update and the optimality peek (as oracle/lpo.c).
+static int solve_dual_deferred(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
+    const Geo g = geo(c);
+    const Launch L = lau(c);
+    const int nrc = pivot_d_blocks(g, 1, 256), ncp = pivot_d_blocks(g, 0, 256);
+    if (!c->drc) HIPCHK(c, hipMalloc(&c->drc, (size_t)nrc * sizeof(Cand)));
+    if (!c->dcp) HIPCHK(c, hipMalloc(&c->dcp, (size_t)ncp * sizeof(Cand)));
+    HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
+    if (launch_dual_rows(L, g, c->drc, nrc)) return fail(c, LPG_ERR_DEVICE, "dual rows launch failed");
+    c->par = 0;
+    c->booted = false;
+    const bool keep = c->no_reorder;
+    c->no_reorder = true;
+    int rc = 0;
+    auto pivot = [&](bool row_only) {
+        const int s = c->par;
+        const Defer D = defer_of(c, c->pend);
+        const double *Pprev = c->Pbuf + (int64_t)((c->pend + c->defer_k - 1) % c->defer_k) * c->ld;
+        return launch_dual_pivot_d(L, g, c->st, s, c->drc, nrc, c->dcp, ncp, c->P, Pprev, c->C[s ^ 1], c->C[s], D,
+                                   row_only);
+    };
+    int64_t done = 0, batch = 8;
+    while (done < max_pivots) {
+        const int64_t n = std::min(batch, max_pivots - done);
+        if ((rc = ensure_log(c, c->enq + n))) break;
+        for (int64_t q = 0; q < n && !rc; q++) {
+            if (pivot(false)) rc = fail(c, LPG_ERR_DEVICE, "dual pivot launch failed");
+            else if (++c->pend == c->defer_k) rc = flush_launch(c);
+            c->par ^= 1;
+            c->enq++;
+        }
+        if (rc) break;
+        done += n;
+        DevState h;
+        HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (h.slot[c->par].status != LPG_RUNNING) break;
+        batch = std::min<int64_t>(batch * 2, 256);
+    }
+    if (!rc && pivot(true)) rc = fail(c, LPG_ERR_DEVICE, "dual row launch failed");
+    if (!rc && hipMemsetAsync(&c->st->slot[c->par].dpend, 0, sizeof(int64_t), c->stream) != hipSuccess)
+        rc = fail(c, LPG_ERR_DEVICE, "hipMemsetAsync failed");
+    if (!rc) rc = materialize(c);
+    c->no_reorder = keep;
+    if (rc) return rc;
+    DevState h;
+    double z = 0;
+    HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&z, c->T + (c->nloc + c->nobj - 1) * c->ld, sizeof z, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int32_t st = h.slot[c->par].status;
+    lpg_result r;
+    r.status = st == LPG_RUNNING ? LPG_ITER_LIMIT : st;
+    r.rule = LPG_RULE_DANTZIG;
+    r.pivots = h.pivots;
+    r.objective = z;
+    r.entering = h.pivots ? h.last_k : -1;
+    r.leaving = h.pivots ? h.last_r : -1;
+    if (out) *out = r;
+    return 0;
+}
+
 int lpg_solve_dual(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
     if (!c || max_pivots < 0) return fail(c, LPG_ERR_ARG, "lpg_solve_dual: bad arguments");
     if (c->world != 1 || has_comm(c)) return fail(c, LPG_ERR_STATE, "lpg_solve_dual: single rank only");
@@ -1471,6 +1537,7 @@ int lpg_solve_dual(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
     for (int64_t j = 1; j <= c->nact; j++)
         if (obj[j] < -c->eps_opt)
             return fail(c, LPG_ERR_STATE, "lpg_solve_dual: basis not dual feasible (d_%lld = %g)", (long long)j, obj[j]);
+    if (c->defer_k > 0 && c->nobj == 1) return solve_dual_deferred(c, max_pivots, out);
     const Geo g = geo(c);
     const Launch L = lau(c);
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
@@ -1498,6 +1565,9 @@ int lpg_solve_dual(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
         if (h.slot[c->par].status != LPG_RUNNING) break;
         batch = std::min<int64_t>(batch * 2, 256);
     }
+    // the budget ran out: k_dual_price alone says whether the last pivot was optimal
+    if (launch_dual_pivot(L, g, c->st, c->par, c->part, c->nsel, c->pp, c->pc, c->npp, c->skip, c->P, c->C[c->par], true))
+        return fail(c, LPG_ERR_DEVICE, "dual price launch failed");
     DevState h;
     double z = 0;
     HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));

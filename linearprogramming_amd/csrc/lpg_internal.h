@@ -39,7 +39,7 @@ struct Slot {                 // 32 B
     int64_t r;                // leaving row (global)
     int32_t status;
     int32_t pad0;
-    int64_t pad1;
+    int64_t dpend;            // dual deferred path: the objective row owes the previous pivot's update (lpg_dual.hip)
 };
 
 struct DevState {
@@ -227,8 +227,17 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
                   int64_t *basis, int64_t *logk, int64_t *logr, int variant, int skip);
 
 int launch_dual_rows(const Launch &L, const Geo &g, Cand *part, int nsel);
+// The dual simplex on the deferred tableau (lpg_dual.hip): k_dual_row_d over
+// npp = pivot_d_blocks(g, 0, 256) column blocks, then k_dual_col_d over npp +
+// nrc (= pivot_d_blocks(g, 1, 256)) blocks. rc: row candidates (in / out), cp:
+// ratio-test partials, R: the current pivot row, Pprev / Cprev: the previous
+// pivot's P and column (its objective update), Cs: this pivot's column.
+// row_only: k_dual_row_d alone (the owed objective update and the final peek).
+int launch_dual_pivot_d(const Launch &L, const Geo &g, DevState *st, int s, Cand *rc, int nrc, Cand *cp, int npp,
+                        double *R, const double *Pprev, const double *Cprev, double *Cs, const Defer &D,
+                        bool row_only);
 int launch_dual_pivot(const Launch &L, const Geo &g, DevState *st, int s, Cand *part, int nsel, PricePart *pp,
-                      int *pc, int npp, int skip, double *P, double *Cs);
+                      int *pc, int npp, int skip, double *P, double *Cs, bool price_only = false);
 
 #ifdef LPG_PHASES
 int debug_phases(unsigned long long *out, int reset);   // tools/phase_probe.py

@@ -1429,10 +1429,10 @@ int launch_dual_rows(const Launch &L, const Geo &g, Cand *part, int nsel) {
 }
 
 int launch_dual_pivot(const Launch &L, const Geo &g, DevState *st, int s, Cand *part, int nsel, PricePart *pp,
-                      int *pc, int npp, int skip, double *P, double *Cs) {
+                      int *pc, int npp, int skip, double *P, double *Cs, bool price_only) {
     hipStream_t stream = (hipStream_t)L.stream;
     hipLaunchKernelGGL(k_dual_price, dim3(npp), dim3(kBlock), 0, stream, g.T, g, st, s, part, nsel, pp, pc);
-    hipLaunchKernelGGL(k_dual_prep, dim3(npp + nsel), dim3(kBlock), 0, stream, g.T, g, st, s, s ^ 1, pp, npp, pc,
+    if (!price_only) hipLaunchKernelGGL(k_dual_prep, dim3(npp + nsel), dim3(kBlock), 0, stream, g.T, g, st, s, s ^ 1, pp, npp, pc,
                        skip, P, Cs, part);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -2362,7 +2362,12 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
         // k_flushw: 4-wave blocks, 128-column x 512-row items swept in 16-row
         // bands with a 2-deep LDS ring of multipliers; small tableaus shrink
         // the items until they fill the chip
-        const int64_t ntiles = (g.ncols + 127) / 128;
+        // 64 slots: 8-wave blocks over 256-column tiles (one B fragment load
+        // per 8 waves instead of 4; config 3: 25.25k vs 25.04k pivots/s,
+        // interleaved A/B, profiles/r03_ab_flushw_wpb8.log)
+        constexpr int kW64 = 8;
+        const int tw = kmax == 64 ? 32 * kW64 : 128;   // tile width: 32 columns per wave
+        const int64_t ntiles = (g.ncols + tw - 1) / tw;
         // (taller items measured at config 4: 1024 / 2048 rows within 1% of 512;
         // 128 rows 13% slower)
         int64_t rows = 512;
@@ -2375,8 +2380,8 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
             hipLaunchKernelGGL((k_flushw<128, 2, 1, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
                                D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
         else if (kmax == 64)
-            hipLaunchKernelGGL((k_flushw<64, 2, 2, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
-                               D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
+            hipLaunchKernelGGL((k_flushw<64, 2, 2, kW64>), dim3((unsigned)((nblocks + 1) / 2)), dim3(64 * kW64), 0, stream,
+                               g.T, g, st, D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
         else
             hipLaunchKernelGGL((k_flushw<32, 2, 3, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
                                D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);

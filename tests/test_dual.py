@@ -3,6 +3,8 @@ wrong label and does nothing; LPStandardize(model, 1) flips every >= row so the
 slack basis is dual feasible, Source/simplex.c:178-179)."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 
@@ -46,10 +48,20 @@ def lpg():
     return lpg
 
 
+def _flags(lpg, path):
+    from linearprogramming_amd import _lib
+    return _lib.FLAG_EAGER if path == "eager" else 0
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["eager", "deferred"])
 @pytest.mark.parametrize("m,n", [(5, 7), (100, 150), (400, 300), (2000, 1500)])
-def test_gpu_dual_bitwise(lpg, m, n):
-    e = lpg.Engine(m, n + m + 1)
+def test_gpu_dual_bitwise(lpg, m, n, path):
+    """Both device forms of the dual: rank-1 updates every pivot (eager) and
+    the deferred blocks (lpg_dual.hip: two kernels per pivot, the block pass
+    every defer_k pivots)."""
+    e = lpg.Engine(m, n + m + 1, flags=_flags(lpg, path))
+    assert (e.info.defer_k == 0) == (path == "eager")
     e.generate(n, 3, lpg.GEN_DUAL)
     o = Oracle(m, n + m + 1)
     o.generate(n, 3, GEN_DUAL)
@@ -60,6 +72,64 @@ def test_gpu_dual_bitwise(lpg, m, n):
     ok, orr = o.get_log()
     assert np.array_equal(ek, ok) and np.array_equal(er, orr)
     assert np.array_equal(e.get_rows(0, m + 1), o.get_rows())
+    assert np.array_equal(e.get_basis(), o.get_basis())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["eager", "deferred"])
+def test_gpu_dual_budget_and_resume(lpg, path):
+    """ITER_LIMIT when the budget runs out first, OPTIMAL when the last pivot of
+    the budget reaches optimality (the final peek, as the oracle), and a second
+    call that resumes where the first stopped (mid-block on the deferred path:
+    the objective row's owed update and the pending pivots are settled first)."""
+    m, n = 400, 300
+    o = Oracle(m, n + m + 1)
+    o.generate(n, 3, GEN_DUAL)
+    total = o.solve_dual(100_000).pivots
+    assert total > 40
+    for cut in (total - 1, total, 37):
+        e = lpg.Engine(m, n + m + 1, flags=_flags(lpg, path))
+        e.generate(n, 3, lpg.GEN_DUAL)
+        oc = Oracle(m, n + m + 1)
+        oc.generate(n, 3, GEN_DUAL)
+        r, rc = e.solve_dual(cut), oc.solve_dual(cut)
+        assert r.status == rc.status == STATUS["OPTIMAL" if cut == total else "ITER_LIMIT"]
+        assert r.pivots == rc.pivots == cut and r.objective == rc.objective
+        assert np.array_equal(e.get_rows(0, m + 1), oc.get_rows())
+        r2, rc2 = e.solve_dual(100_000), oc.solve_dual(100_000)
+        assert r2.status == rc2.status == STATUS["OPTIMAL"] and r2.pivots == rc2.pivots == total
+        assert r2.objective == rc2.objective
+        assert np.array_equal(e.get_rows(0, m + 1), oc.get_rows())
+
+
+@pytest.mark.gpu
+def test_gpu_dual_deferred_full_size(lpg):
+    """LPG_GEN_DUAL at 16384 x 16384 (4.3 GB, 64-pivot blocks): 200 dual pivots
+    = three whole blocks and a partial one settled by the readout, bitwise
+    against the C oracle (log, basis, objective row, column 0, every pivot row
+    and 64 sampled rows)."""
+    m = n = 16384
+    piv = 200
+    e = lpg.Engine(m, n + m + 1)
+    assert e.info.defer_k == 64
+    e.generate(n, 7, lpg.GEN_DUAL)
+    e.reserve_log(piv + 8)
+    r = e.solve_dual(piv)
+    o = Oracle(m, n + m + 1, nthreads=min(16, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    o.generate(n, 7, GEN_DUAL)
+    ro = o.solve_dual(piv)
+    assert r.status == ro.status == STATUS["ITER_LIMIT"] and r.pivots == ro.pivots == piv
+    assert r.objective == ro.objective
+    ek, er = e.get_log()
+    ok, orr = o.get_log()
+    assert np.array_equal(ek, ok) and np.array_equal(er, orr)
+    assert np.array_equal(e.get_basis(), o.get_basis())
+    assert np.array_equal(e.get_rows(m, 1), o.get_rows(m, 1))
+    assert np.array_equal(e.get_column0(), np.concatenate([o.get_rows(i0, 1024)[:, 0] for i0 in range(0, m, 1024)]))
+    rng = np.random.default_rng(1)
+    for i in sorted(set(int(x) for x in orr) | set(rng.choice(m, 64, replace=False).tolist())):
+        assert np.array_equal(e.get_rows(i, 1), o.get_rows(i, 1)), f"row {i}"
+    e.close()
 
 
 @pytest.mark.gpu

@@ -137,8 +137,10 @@ def _random_lp_rich(rng):
 
 def _reference_aligned(path):
     """The reference binary's tableau after LPAlign; None if it rejected the
-    model, "crash" if it died first (heap corruption in its term arrays on some
-    models with free variables: `realloc(): invalid next size`)."""
+    model, "crash" if it died first (CreateSMatrix writes its lack list through
+    `*lack[lackPtr++]`, matrix.c:86, a wild pointer once two rows lack a unit
+    column; on some models with free variables heap corruption in its term
+    arrays: `realloc(): invalid next size`)."""
     p = subprocess.run([REF, path], input="\n1\n\n\n1\n\n\nq\n", capture_output=True, text=True, timeout=20,
                        cwd=ROOT, env={"TERM": "dumb", "PATH": "/usr/bin:/bin"})
     models = refparse.parse_models(p.stdout)
@@ -206,13 +208,14 @@ SAN_CLI = os.path.join(ROOT, "integration", "_san", "lpgcli")
 needs_cli = pytest.mark.skipif(not os.path.exists(CLI), reason="host/lpgcli not built")
 
 
-def _c_dump(path, cli=CLI):
-    p = subprocess.run([cli, "--lp-dump", path], capture_output=True, text=True, timeout=30)
+def _c_dump(path, cli=CLI, dual=False):
+    p = subprocess.run([cli, "--lp-dump", path] + (["--dual"] if dual else []), capture_output=True, text=True,
+                       timeout=30)
     return p.returncode, json.loads(p.stdout)
 
 
-def _py_dump(text):
-    sm = F.build_smatrix(text)
+def _py_dump(text, dual=False):
+    sm = F.build_smatrix(text, dual=dual)
     return {"names": sm.display_names, "basis": sm.basis, "costs": [f"{c.numerator}/{c.denominator}" for c in sm.costs],
             "constant": f"{sm.constant.numerator}/{sm.constant.denominator}",
             "zcoef": f"{sm.zcoef.numerator}/{sm.zcoef.denominator}",
@@ -236,6 +239,28 @@ def test_c_front_end_equals_the_python_one(tmp_path):
         rc, got = _c_dump(f)
         try:
             exp = _py_dump(text)
+        except F.FrontendError as ex:
+            assert rc == 3 and "error" in got, (f, got, str(ex))
+            continue
+        assert rc == 0 and got == exp, (text, got, exp)
+
+
+@needs_cli
+def test_c_front_end_dual_form_equals_the_python_one(tmp_path):
+    """LPStandardize's dual form (simplex.c:178-179, lpgcli --lp-dump MODEL --dual)
+    in both restatements: the fixtures, 100 random dual-feasible models and 100
+    general ones."""
+    files = [os.path.join(LP, f) for f in sorted(os.listdir(LP))]
+    rng = np.random.default_rng(17)
+    for t in range(200):
+        f = tmp_path / f"d{t}.txt"
+        f.write_text(_random_dual_lp(rng) if t < 100 else _random_lp_rich(rng))
+        files.append(str(f))
+    for f in files:
+        text = open(f).read()
+        rc, got = _c_dump(f, dual=True)
+        try:
+            exp = _py_dump(text, dual=True)
         except F.FrontendError as ex:
             assert rc == 3 and "error" in got, (f, got, str(ex))
             continue

@@ -96,3 +96,50 @@ def test_gpus_config3_pair_path():
     dist = json.loads(lp[0])
     assert dist["pivots"] == one["pivots"] == 200 and dist["objective"] == one["objective"]
     assert dist["log_fnv"] == one["log_fnv"] and dist["pivot_wg"] == 0
+
+
+DUAL_LP = "OF {\n\tmin:z=2x1+3x2\n}\nST {\n\tx1+x2>=4;\n\tx1+3x2>=6;\n\tx1>=0;\n\tx2>=0\n}\n"
+
+
+@needs_cli
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n", [(400, 300), (2000, 1500)])
+def test_cli_dual_synthetic_equals_the_oracle(m, n):
+    """lpgcli --synthetic M N --dual: LPG_GEN_DUAL through lpg_solve_dual (the
+    deferred blocks at these sizes) from plain C, against the oracle's dual."""
+    p, lines = _cli(["--synthetic", str(m), str(n), "--dual", "--seed", "3"])
+    assert p.returncode == 0, p.stderr
+    got = json.loads(lines[-1])
+    assert got["method"] == "dual" and got["defer_k"] > 0
+    o = Oracle(m, n + m + 1)
+    o.generate(n, 3, 3)
+    res = o.solve_dual(1 << 40)
+    assert got["status"] == "OPTIMAL" and res.status == 1
+    assert got["pivots"] == res.pivots and got["objective"] == res.objective
+    assert got["log_fnv"] == _fnv(*o.get_log())
+
+
+@needs_cli
+@pytest.mark.gpu
+def test_cli_dual_lp_model(tmp_path):
+    """lpgcli --lp MODEL --dual: the dual form from the C front end, solved by the
+    dual simplex on the device; the same optimum as the primal two-phase run and
+    as the Python front end's dual."""
+    from linearprogramming_amd import frontend as F
+    f = tmp_path / "dual.txt"
+    f.write_text(DUAL_LP)
+    p, lines = _cli(["--lp", str(f), "--dual"])
+    assert p.returncode == 0, p.stderr
+    dual = json.loads(lines[-1])
+    p, lines = _cli(["--lp", str(f)])
+    primal = json.loads(lines[-1])
+    assert dual["status"] == primal["status"] == "OPTIMAL"
+    assert abs(dual["z"] - 9.0) < 1e-12 and abs(primal["z"] - 9.0) < 1e-12
+    assert {v: dual["variables"][v] for v in ("x1", "x2")} == pytest.approx({"x1": 3.0, "x2": 1.0}, abs=1e-12)
+    py = F.solve_text(DUAL_LP, method="dual")
+    assert py.status == "OPTIMAL" and py.pivots == dual["pivots"] and py.z == dual["z"]
+    # not dual feasible (a positive max-form cost): a clean error line
+    g = tmp_path / "notdual.txt"
+    g.write_text("OF {\n\tmax:z=x1\n}\nST {\n\tx1<=3;\n\tx1>=0\n}\n")
+    p, lines = _cli(["--lp", str(g), "--dual"])
+    assert p.returncode != 0 and "dual feasible" in json.loads(lines[-1])["error"]
