@@ -71,14 +71,9 @@ constexpr int kMaxWG = 256;         // records swept per phase: 4 per lane of on
 constexpr int kPer = kMaxWG / 64;
 constexpr int kRecPMax = 5;         // pricing record granules (k_pivot_block's NGP), space reserved per workgroup
 constexpr int kRecR = 2;            // ratio record:   {theta, key, tag} {piv, row, tag}
-#ifndef LPG_MAX_LDS_KB
-#define LPG_MAX_LDS_KB 150          // experiments: the dynamic LDS cap (the slices) in KB
-#endif
-constexpr int kMaxLds = LPG_MAX_LDS_KB * 1024;   // dynamic LDS cap (the slices)
+constexpr int kMaxLds = 150 * 1024;  // dynamic LDS cap (the slices)
 constexpr long long kSpinTicks = 200000000ll;   // s_memrealtime runs at 100 MHz: 2 s
-#ifndef LPG_SWEEP_SLEEP
-#define LPG_SWEEP_SLEEP 1           // s_sleep between record polls (64 clocks each)
-#endif
+constexpr int kSweepSleep = 1;      // s_sleep between record polls (64 clocks each)
 
 // doubles per thread row of the LDS slices: the unrolled chains read 16, 32,
 // 48 or 64 slots, so >= ks rounded up to 16; = 2 mod 4 (16-byte reads at this
@@ -88,18 +83,13 @@ __host__ __device__ constexpr int slot_stride(int ks) { return ((ks + 15) & ~15)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, int bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, bytes, 0x00020000);
 }
-// ONE 16-byte write-through store / load (aux 16 = sc1; LPG_REC_*_AUX: experiments)
-#ifndef LPG_REC_ST_AUX
-#define LPG_REC_ST_AUX 16
-#endif
-#ifndef LPG_REC_LD_AUX
-#define LPG_REC_LD_AUX 16
-#endif
+// ONE 16-byte write-through store / load (aux 16 = sc1)
+constexpr int kRecAux = 16;
 __device__ __forceinline__ void rec_store(__amdgpu_buffer_rsrc_t r, int off, u4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, LPG_REC_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kRecAux);
 }
 __device__ __forceinline__ u4 rec_load(__amdgpu_buffer_rsrc_t r, int off) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, LPG_REC_LD_AUX);
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kRecAux);
 }
 // 8-byte write-through store / load of a double (global_store/load_dwordx2 sc1)
 __device__ __forceinline__ void st_wt(double *p, double v) {
@@ -165,7 +155,7 @@ __device__ bool sweep(__amdgpu_buffer_rsrc_t r, int nwg, uint32_t tag, u4 (&rec)
             }
             return false;
         }
-        __builtin_amdgcn_s_sleep(LPG_SWEEP_SLEEP);
+        __builtin_amdgcn_s_sleep(kSweepSleep);
     }
 }
 
@@ -712,27 +702,8 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         // k_prep_d's bookkeeping, stores only (a dependent load here would hold
         // back workgroup 0, and every sweep waits for the slowest workgroup):
         // the row's owner records the leaving variable it holds
-#ifndef LPG_BOOK_LATE
-#define LPG_BOOK_LATE 0             // experiments: 1 = single-rank bookkeeping by wave 1 after the pricing record
-#endif
-        auto bookkeeping = [&]() {
-            st->slot[s].r = r;
-            D.rq[q] = rl;
-            st->npend = q + 1;
-            D.kq[q] = kt;
-            D.pv[q] = piv;
-            const int64_t np = np0 + t;
-            if (D.logk && np < logcap) {
-                D.logk[np] = kt;
-                D.logr[np] = r;
-            }
-            st->pivots = np + 1;
-            st->last_k = kt;
-            st->last_r = r;
-        };
-        if (!MR && LPG_BOOK_LATE) {
-            // below, after this workgroup's pricing record
-        } else if (wg == 0 && tid == 0) {
+        // (moving it to wave 1 after the pricing record measured nothing)
+        if (wg == 0 && tid == 0) {
             st->slot[s].r = r;
             D.rq[q] = rl;
             if (MR) lvv = D.basis[r];                   // stored after the P exchange: its latency hides there
@@ -835,7 +806,6 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             rec_store(recP, (wg * NGP + 2) * 16, pack(0ull, 0u, tag));
             if (NOBJ == 2) rec_store(recP, (wg * NGP + 4) * 16, pack(0ull, 0u, tag));
         }
-        if (!MR && LPG_BOOK_LATE && wg == 0 && tid == 64) bookkeeping();   // nothing in the launch reads it
         LPG_BPUB(0, t);
         LPG_BPH(t, 3);
 

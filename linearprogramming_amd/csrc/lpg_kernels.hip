@@ -1832,9 +1832,6 @@ __global__ __launch_bounds__(kBlock, LB > 0 ? LB : 1) void k_flushm(double *__re
 // WPB waves per block: a tile is 32 * WPB columns wide, and every column
 // tile reads all of C once (WPB = 8 halves that on-chip traffic: C is
 // 8.4 MB at config 3, read by every tile from the Infinity Cache).
-#ifndef LPG_FLUSHW_DEPTH
-#define LPG_FLUSHW_DEPTH 1            // tableau bands loaded ahead of the one on the matrix cores
-#endif
 template <int KMAX, int NB, int LB, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T, Geo g, DevState *__restrict__ st,
                                                          const double *__restrict__ Pbuf,
@@ -1926,19 +1923,9 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T,
         };
         d2 t[4];
         tload(t, 0);
-#if LPG_FLUSHW_DEPTH > 1
-        d2 tq[4];                             // experiments: tableau bands two ahead
-        if (1 < nb) tload(tq, 1);
-#endif
         for (int s = 0; s < nb; s++) {
-            d2 tn[4];
-#if LPG_FLUSHW_DEPTH > 1
-#pragma unroll
-            for (int r = 0; r < 4; r++) tn[r] = tq[r];
-            if (s + 2 < nb) tload(tq, s + 2);
-#else
+            d2 tn[4];                         // one band ahead (two ahead measured no faster)
             if (s + 1 < nb) tload(tn, s + 1);
-#endif
             __syncthreads();                  // band s is staged; ring slot (s - 1) % NB is free
             cstore(cn, s + NB - 1);
             cload(cn, s + NB);

@@ -9,7 +9,14 @@
 #   pmc:NAME:CTR:ARGS  one rocprofv3 --pmc pass (CTR) of bench.py ARGS -> gpurun_out/pmc_NAME/
 #   py:NAME:ARGS       python ARGS                   -> gpurun_out/py_NAME.log
 #   smoke:NAME:        __graft_entry__.smoke()       -> gpurun_out/smoke_NAME.log
+#   ab:NAME:LIBS       config-3 pivots/s of the in-tree liblpg and each .so in LIBS,
+#                      interleaved twice (tools/sweep_exp.py) -> gpurun_out/ab_NAME.log
+#   run:NAME:CMD       any other command (lab binaries such as tools/flush_lab,
+#                      env-var sweeps: "run:x:env LPG_DEFER=32 python bench.py")
+#                                                    -> gpurun_out/run_NAME.log
 # Limits: T_PYTEST (900 s), T_BENCH (300 s), T_PY (300 s).
+# Profiles: "prof:c3:--steps 2 --warmup 0 --no-cpu", then one pmc step per
+# counter group, e.g. "pmc:fetch:FETCH_SIZE:--steps 2 --warmup 0 --no-cpu".
 # Example: gpurun --timeout 1200 -- bash tools/gpu.sh "pytest:all:tests -m gpu -x -q" "bench:c3:--steps 20"
 set -u
 export TMPDIR=/tmp
@@ -47,6 +54,17 @@ for spec in "$@"; do
             timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "gpurun_out/smoke_$name.log" 2>&1 \
                 || { tail -20 "gpurun_out/smoke_$name.log"; exit 1; }
             tail -2 "gpurun_out/smoke_$name.log" ;;
+        ab)
+            : > "gpurun_out/ab_$name.log"
+            for lib in "" $args "" $args; do
+                timeout -k 10 "${T_PY:-300}" python -u tools/sweep_exp.py $lib >> "gpurun_out/ab_$name.log" 2>&1 \
+                    || { tail -30 "gpurun_out/ab_$name.log"; exit 1; }
+            done
+            grep pivots/s "gpurun_out/ab_$name.log" ;;
+        run)
+            timeout -k 10 "${T_PY:-300}" $args > "gpurun_out/run_$name.log" 2>&1 \
+                || { tail -30 "gpurun_out/run_$name.log"; exit 1; }
+            tail -5 "gpurun_out/run_$name.log" ;;
         *)
             echo "unknown step kind: $kind" >&2
             exit 2 ;;
