@@ -22,6 +22,20 @@
 // ahead: 3.00-3.02 ms; 3- or 4-deep multiplier rings: 3.02-3.08 ms
 // (profiles/r02_flush_lab_k128_apre.log, _ring.log): the loop sits at ~46
 // TFLOP/s whatever feeds it.
+//
+// Round 3 (profiles/r03_flush_lab_k128_v.log, _s.log, r03_mfma_rate2.log):
+// an MFMA chain with A from LDS and B from a register array reaches 67-74
+// TFLOP/s at 1-4 waves per SIMD, and 69 TFLOP/s while other waves of the same
+// CUs stream 3.5 TB/s of HBM read-modify-write -- the pipe and the memory
+// system do overlap. The passes still sit at 46-47: k_flushv (16-column wave
+// tiles, one chain per wave, 8 or 16 waves per block, 2 or 4 per SIMD)
+// 2.92-2.98 ms; k_flushs (loader waves moving tableau bands and multipliers
+// into a 4-deep LDS ring by LDS-DMA, matrix waves only computing, one bare
+// barrier per band) 3.25-3.79 ms, its data path alone 2.04 ms and its matrix
+// path alone 2.69 ms (51 TFLOP/s: the per-band barrier of 12 waves). At
+// config 4 on one GPU k_flushv<128,2,16> loses to k_flushw<128> (48.6 vs
+// 47.5 ms per 128-pivot pass, profiles/r03_bench_config4_flushw_vs_flushv.log),
+// so neither is in the product.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o tools/flush_lab tools/flush_lab.hip
 //   tools/flush_lab [rows]            (LAB_ONLY=substring picks designs)
 #include "../linearprogramming_amd/csrc/lpg_kernels.hip"
@@ -40,6 +54,267 @@
     } while (0)
 
 namespace lpg {
+
+// k_flushv: k_flushw with 16-column wave tiles, ONE MFMA chain per wave and B
+// (32 doubles per lane at 128 slots) in VGPRs, so that a wave needs about
+// half the registers and WPB = 16 waves per block put 4 waves on each SIMD:
+// at 128 slots k_flushw runs 1 wave per SIMD (256 VGPRs + AGPRs), and that
+// single issue stream, not the operands, held its matrix cores at ~46 of the
+// ~75 TFLOP/s the f64 MFMA pipe reaches (tools/flush_lab.hip). Lane (lk, lc)
+// holds column lc of its wave's 16 and rows lk + 4r of the band; the chain,
+// the multiplier ring and the dynamic item queue are k_flushw's, so the
+// results are the same per-element fma chain (the skipping is per column
+// here, per column pair there: they differ at most in the sign of a zero).
+template <int KMAX, int NB, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_flushv(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                     const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
+                                                     int64_t cs, int64_t ntiles, int64_t nitems, int64_t rows,
+                                                     int skip) {
+    constexpr int NTH = 64 * WPB;
+    constexpr int G = KMAX / 4;
+    constexpr int BAND = KMAX * 16;                 // doubles per band
+    constexpr int NPC = BAND / 2;                   // 16-byte multiplier pieces per band
+    constexpr int PER = (NPC + NTH - 1) / NTH;      // ... per thread
+    __shared__ __attribute__((aligned(16))) double sC[NB][BAND];
+    __shared__ int64_t next_item;
+    __shared__ int wsum[WPB];
+    const int np = (int)st->npend;
+    if (np <= 0) return;
+    const int64_t ld = g.ld;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lc = lane & 15, lk = lane >> 4;
+    unsigned long long touched = 0;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
+        __syncthreads();
+        const int64_t item = next_item;
+        if (item >= nitems) break;
+        const int64_t tile = item % ntiles, strip = item / ntiles;
+        const int64_t i0 = strip * rows;
+        const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
+        const int64_t cl = tile * (16 * WPB) + wave * 16 + lc;      // this lane's column
+        const bool in = cl < g.ncols;
+        double b[G];
+        bool live = false;
+#pragma unroll
+        for (int gq = 0; gq < G; gq++) {
+            const int q = 4 * gq + lk;
+            const double v = (in && q < np) ? Pbuf[(int64_t)q * ld + cl] : 0.0;
+            b[gq] = v;
+            live = live || v != 0.0;
+        }
+        live = (__shfl_xor((int)live, 16, 64) | (int)live) != 0;     // OR over the 4 lanes of the column
+        live = (__shfl_xor((int)live, 32, 64) | (int)live) != 0;
+        const bool ok = in && (!skip || live);
+        int mine = (lk == 0 && ok) ? 1 : 0;
+        for (int mask = 32; mask > 0; mask >>= 1) mine += __shfl_xor(mine, mask, 64);
+        const bool wlive = mine > 0;                                   // wave-uniform
+        if (lane == 0) wsum[wave] = mine;
+        if (__syncthreads_count(wlive && lane == 0) == 0) continue;    // the whole tile is skipped
+        if (threadIdx.x == 0) {
+            int sum = 0;
+#pragma unroll
+            for (int w = 0; w < WPB; w++) sum += wsum[w];
+            touched += (unsigned long long)sum * (unsigned long long)(i1 - i0);
+        }
+        const int nb = (int)((i1 - i0 + 15) / 16);
+        auto cload = [&](d2 (&cr)[PER], int s) {
+#pragma unroll
+            for (int u = 0; u < PER; u++) {
+                const int e = threadIdx.x + u * NTH;
+                const int q = e >> 3, rr = 2 * (e & 7);
+                const int64_t row = i0 + 16 * s + rr;
+                d2 v = d2{0.0, 0.0};
+                if (e < NPC && s < nb && q < np && row < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + row);
+                cr[u] = -v;
+            }
+        };
+        auto cstore = [&](const d2 (&cr)[PER], int s) {
+#pragma unroll
+            for (int u = 0; u < PER; u++) {
+                const int e = threadIdx.x + u * NTH;
+                if (e < NPC) *(d2 *)(&sC[s % NB][2 * e]) = cr[u];
+            }
+        };
+        for (int s = 0; s < NB - 1; s++) {
+            d2 cr[PER];
+            cload(cr, s);
+            cstore(cr, s);
+        }
+        d2 cn[PER];
+        cload(cn, NB - 1);
+        auto tload = [&](double (&x)[4], int s) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int64_t row = i0 + 16 * s + lk + 4 * r;
+                x[r] = (ok && row < i1) ? __builtin_nontemporal_load(T + row * ld + cl) : 0.0;
+            }
+        };
+        double t[4];
+        tload(t, 0);
+        for (int s = 0; s < nb; s++) {
+            double tn[4];
+            if (s + 1 < nb) tload(tn, s + 1);
+            __syncthreads();                  // band s is staged; ring slot (s - 1) % NB is free
+            cstore(cn, s + NB - 1);
+            cload(cn, s + NB);
+            if (wlive) {
+                d4 acc = d4{t[0], t[1], t[2], t[3]};
+                const double *sa = &sC[s % NB][lk * 16 + lc];
+#pragma unroll
+                for (int gq = 0; gq < G; gq++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[gq * 64], b[gq], acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = i0 + 16 * s + lk + 4 * r;
+                    if (ok && row < i1) __builtin_nontemporal_store(acc[r], T + row * ld + cl);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) t[r] = tn[r];
+        }
+    }
+    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
+}
+
+
+// k_flushs: the block pass with specialised waves. At 128 slots the pass is
+// balanced (16 flop per tableau byte against the box's ~14.5 = 74 TFLOP/s /
+// 5.1 TB/s), and k_flushw / k_flushv, whose waves each load, compute and
+// store in turn, overlap the two streams badly (46-47 TFLOP/s, 2.9-3.0 ms at
+// the config-3 shape, while an MFMA loop reaches ~69 TFLOP/s with an HBM
+// stream of 3.5 TB/s running beside it on the same CUs: tools/mfma_rate2.hip).
+// Here LW loader waves only move data: tableau bands (16 rows x 16*MW
+// columns) and the band's multipliers go from HBM / the Infinity Cache into
+// an LDS ring by LDS-DMA (global_load_lds, 16 B per lane, no registers), DT
+// bands ahead; MW matrix waves only compute: each takes 16 columns (k_flushv's
+// lane map), its accumulators from the ring, the chain on the matrix cores
+// with B = -P in VGPRs, and stores the results. One barrier per band hands
+// the ring on. Multipliers are raw C with B negated: fma(c, -p, x) ==
+// fma(-c, p, x) bit for bit, and padding slots are A = +0 (the zero row) with
+// B = -0, x + (+0)(-0) == x for every x: the same chain as every other pass.
+template <int KMAX, int MW, int LW, int DT>
+__global__ __launch_bounds__(64 * (MW + LW)) void k_flushs(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                           const double *__restrict__ Pbuf,
+                                                           const double *__restrict__ Cbuf, int64_t cs, int64_t ntiles,
+                                                           int64_t nitems, int64_t rows, int skip,
+                                                           const double *__restrict__ zrow) {
+    constexpr int G = KMAX / 4;
+    constexpr int TW = 16 * MW;                     // tile width (columns)
+    constexpr int RING = DT + 1;
+    constexpr int TB = 16 * TW;                     // doubles of tableau per band
+    constexpr int CB = 16 * KMAX;                   // doubles of multipliers per band
+    constexpr int SLOT = TB + CB;
+    constexpr int NT_DMA = TB / 128;                // 1 KB DMA instructions per band: tableau ...
+    constexpr int NC_DMA = CB / 128;                // ... and multipliers
+    static_assert(TW == 128 && NT_DMA % LW == 0 && NC_DMA % LW == 0, "one 1 KB row per tableau DMA");
+    constexpr int TPW = NT_DMA / LW, CPW = NC_DMA / LW;   // per loader wave
+    extern __shared__ __attribute__((aligned(16))) double ring[];
+    __shared__ int64_t next_item;
+    __shared__ int wsum[MW];
+    const int np = (int)st->npend;
+    if (np <= 0) return;
+    const int64_t ld = g.ld;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool mw = wave < MW;                      // matrix wave (else loader wave wave - MW)
+    const int lw = wave - MW;
+    const int lc = lane & 15, lk = lane >> 4;
+    unsigned long long touched = 0;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
+        __syncthreads();
+        const int64_t item = next_item;
+        if (item >= nitems) break;
+        const int64_t tile = item % ntiles, strip = item / ntiles;
+        const int64_t i0 = strip * rows;
+        const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
+        const int64_t c0 = tile * TW;
+        const int64_t cl = c0 + (mw ? wave * 16 : 0) + lc;          // a matrix lane's column
+        const bool in = mw && cl < g.ncols;
+        double b[G];
+        bool live = false;
+#pragma unroll
+        for (int gq = 0; gq < G; gq++) {
+            const int q = 4 * gq + lk;
+            const double v = (in && q < np) ? Pbuf[(int64_t)q * ld + cl] : 0.0;
+            b[gq] = -v;
+            live = live || v != 0.0;
+        }
+        live = (__shfl_xor((int)live, 16, 64) | (int)live) != 0;
+        live = (__shfl_xor((int)live, 32, 64) | (int)live) != 0;
+        const bool ok = in && (!skip || live);
+        int mine = (lk == 0 && ok) ? 1 : 0;
+        for (int mask = 32; mask > 0; mask >>= 1) mine += __shfl_xor(mine, mask, 64);
+        const bool wlive = mine > 0;                                   // wave-uniform
+        if (mw && lane == 0) wsum[wave] = mine;
+        if (__syncthreads_count(wlive && lane == 0) == 0) continue;    // the whole tile is skipped
+        if (threadIdx.x == 0) {
+            int sum = 0;
+#pragma unroll
+            for (int w = 0; w < MW; w++) sum += wsum[w];
+            touched += (unsigned long long)sum * (unsigned long long)(i1 - i0);
+        }
+        const int nb = (int)((i1 - i0 + 15) / 16);
+        // loader wave: band s into ring slot s % RING (rows past i1 and slots
+        // past np read the zero row; the tableau's last tile reads into the
+        // next row's padding, which the stores never write back)
+        auto issue = [&](int s) {
+            double *slot = ring + (size_t)(s % RING) * SLOT;
+#pragma unroll
+            for (int u = 0; u < TPW; u++) {
+                const int rr = lw * TPW + u;
+                const int64_t row = i0 + 16 * s + rr;
+                const double *src = row < i1 ? T + row * ld + c0 + 2 * lane : zrow + 2 * lane;
+                __builtin_amdgcn_global_load_lds((const void *)src, (void *)(slot + rr * TW), 16, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < CPW; u++) {
+                const int e = lw * CPW + u;                 // 8 slots x 16 rows per instruction
+                const int q = 8 * e + (lane >> 3);
+                const int64_t row = i0 + 16 * s + 2 * (lane & 7);
+                const double *src = (q < np && row < i1) ? Cbuf + (int64_t)q * cs + row : zrow + 2 * lane;
+                __builtin_amdgcn_global_load_lds((const void *)src, (void *)(slot + TB + e * 128), 16, 0, 0);
+            }
+        };
+        if (!mw)
+            for (int s = 0; s < DT && s < nb; s++) issue(s);
+        for (int s = 0; s < nb; s++) {
+            if (!mw) {   // band s has landed (bands s+1 .. s+DT-1 may still be in flight)
+                if (s + DT - 1 < nb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DT - 1) * (TPW + CPW)) : "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            // band s is in the ring; slot (s - 1) % RING is free. A bare
+            // s_barrier: __syncthreads() would also wait for every wave's
+            // outstanding memory operations (vmcnt(0)), i.e. drain the DMA
+            // ring and the matrix waves' stores each band
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (!mw) {
+                if (s + DT < nb) issue(s + DT);
+            } else if (wlive) {
+                const double *slot = ring + (size_t)(s % RING) * SLOT;
+                d4 acc;
+#pragma unroll
+                for (int r = 0; r < 4; r++) acc[r] = slot[(lk + 4 * r) * TW + wave * 16 + lc];
+                const double *sa = slot + TB + lk * 16 + lc;
+#pragma unroll
+                for (int gq = 0; gq < G; gq++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[gq * 64], b[gq], acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = i0 + 16 * s + lk + 4 * r;
+                    if (ok && row < i1) __builtin_nontemporal_store(acc[r], T + row * ld + cl);
+                }
+            }
+        }
+    }
+    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
+}
+
+template <int KMAX>
+constexpr size_t flushs_lds() { return (size_t)4 * (16 * 128 + 16 * KMAX) * sizeof(double); }   // DT = 3
+
 
 // k_flushx: 128-slot blocks. Wave tile 32 columns (16-byte accesses, even /
 // odd-column MFMA chains as k_flushw) x SB bands of 16 rows per step, so a
@@ -319,6 +594,242 @@ __global__ __launch_bounds__(256, LB) void k_flushy(double *__restrict__ T, Geo 
     if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
 }
 
+// probe modes: 1 = no multiplier staging (ring left as is), 2 = no tableau loads / stores,
+// 3 = no block barrier per band (timing only)
+template <int KMAX, int NB, int WPB, int MODE>
+__global__ __launch_bounds__(64 * WPB) void k_flushv_probe(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                     const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
+                                                     int64_t cs, int64_t ntiles, int64_t nitems, int64_t rows,
+                                                     int skip) {
+    constexpr int NTH = 64 * WPB;
+    constexpr int G = KMAX / 4;
+    constexpr int BAND = KMAX * 16;                 // doubles per band
+    constexpr int NPC = BAND / 2;                   // 16-byte multiplier pieces per band
+    constexpr int PER = (NPC + NTH - 1) / NTH;      // ... per thread
+    __shared__ __attribute__((aligned(16))) double sC[NB][BAND];
+    __shared__ int64_t next_item;
+    __shared__ int wsum[WPB];
+    const int np = (int)st->npend;
+    if (np <= 0) return;
+    const int64_t ld = g.ld;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lc = lane & 15, lk = lane >> 4;
+    unsigned long long touched = 0;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
+        __syncthreads();
+        const int64_t item = next_item;
+        if (item >= nitems) break;
+        const int64_t tile = item % ntiles, strip = item / ntiles;
+        const int64_t i0 = strip * rows;
+        const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
+        const int64_t cl = tile * (16 * WPB) + wave * 16 + lc;      // this lane's column
+        const bool in = cl < g.ncols;
+        double b[G];
+        bool live = false;
+#pragma unroll
+        for (int gq = 0; gq < G; gq++) {
+            const int q = 4 * gq + lk;
+            const double v = (in && q < np) ? Pbuf[(int64_t)q * ld + cl] : 0.0;
+            b[gq] = v;
+            live = live || v != 0.0;
+        }
+        live = (__shfl_xor((int)live, 16, 64) | (int)live) != 0;     // OR over the 4 lanes of the column
+        live = (__shfl_xor((int)live, 32, 64) | (int)live) != 0;
+        const bool ok = in && (!skip || live);
+        int mine = (lk == 0 && ok) ? 1 : 0;
+        for (int mask = 32; mask > 0; mask >>= 1) mine += __shfl_xor(mine, mask, 64);
+        const bool wlive = mine > 0;                                   // wave-uniform
+        if (lane == 0) wsum[wave] = mine;
+        if (__syncthreads_count(wlive && lane == 0) == 0) continue;    // the whole tile is skipped
+        if (threadIdx.x == 0) {
+            int sum = 0;
+#pragma unroll
+            for (int w = 0; w < WPB; w++) sum += wsum[w];
+            touched += (unsigned long long)sum * (unsigned long long)(i1 - i0);
+        }
+        const int nb = (int)((i1 - i0 + 15) / 16);
+        auto cload = [&](d2 (&cr)[PER], int s) {
+#pragma unroll
+            for (int u = 0; u < PER; u++) {
+                const int e = threadIdx.x + u * NTH;
+                const int q = e >> 3, rr = 2 * (e & 7);
+                const int64_t row = i0 + 16 * s + rr;
+                d2 v = d2{0.0, 0.0};
+                if (MODE != 1 && e < NPC && s < nb && q < np && row < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + row);
+                cr[u] = -v;
+            }
+        };
+        auto cstore = [&](const d2 (&cr)[PER], int s) {
+#pragma unroll
+            for (int u = 0; u < PER; u++) {
+                const int e = threadIdx.x + u * NTH;
+                if (MODE != 1 && e < NPC) *(d2 *)(&sC[s % NB][2 * e]) = cr[u];
+            }
+        };
+        for (int s = 0; s < NB - 1; s++) {
+            d2 cr[PER];
+            cload(cr, s);
+            cstore(cr, s);
+        }
+        d2 cn[PER];
+        cload(cn, NB - 1);
+        auto tload = [&](double (&x)[4], int s) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int64_t row = i0 + 16 * s + lk + 4 * r;
+                x[r] = (MODE != 2 && ok && row < i1) ? __builtin_nontemporal_load(T + row * ld + cl) : 0.0;
+            }
+        };
+        double t[4];
+        tload(t, 0);
+        for (int s = 0; s < nb; s++) {
+            double tn[4];
+            if (s + 1 < nb) tload(tn, s + 1);
+            if (MODE != 3) __syncthreads();     // band s is staged; ring slot (s - 1) % NB is free
+            cstore(cn, s + NB - 1);
+            cload(cn, s + NB);
+            if (wlive) {
+                d4 acc = d4{t[0], t[1], t[2], t[3]};
+                const double *sa = &sC[s % NB][lk * 16 + lc];
+#pragma unroll
+                for (int gq = 0; gq < G; gq++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[gq * 64], b[gq], acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = i0 + 16 * s + lk + 4 * r;
+                    if (MODE != 2 && ok && row < i1) __builtin_nontemporal_store(acc[r], T + row * ld + cl);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) t[r] = tn[r];
+        }
+    }
+    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
+}
+
+
+// probe modes (timing only): 1 = no MFMA (the data path alone), 2 = no DMA (the matrix path alone)
+template <int KMAX, int MW, int LW, int DT, int MODE>
+__global__ __launch_bounds__(64 * (MW + LW)) void k_flushs_probe(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                           const double *__restrict__ Pbuf,
+                                                           const double *__restrict__ Cbuf, int64_t cs, int64_t ntiles,
+                                                           int64_t nitems, int64_t rows, int skip,
+                                                           const double *__restrict__ zrow) {
+    constexpr int G = KMAX / 4;
+    constexpr int TW = 16 * MW;                     // tile width (columns)
+    constexpr int RING = DT + 1;
+    constexpr int TB = 16 * TW;                     // doubles of tableau per band
+    constexpr int CB = 16 * KMAX;                   // doubles of multipliers per band
+    constexpr int SLOT = TB + CB;
+    constexpr int NT_DMA = TB / 128;                // 1 KB DMA instructions per band: tableau ...
+    constexpr int NC_DMA = CB / 128;                // ... and multipliers
+    static_assert(TW == 128 && NT_DMA % LW == 0 && NC_DMA % LW == 0, "one 1 KB row per tableau DMA");
+    constexpr int TPW = NT_DMA / LW, CPW = NC_DMA / LW;   // per loader wave
+    extern __shared__ __attribute__((aligned(16))) double ring[];
+    __shared__ int64_t next_item;
+    __shared__ int wsum[MW];
+    const int np = (int)st->npend;
+    if (np <= 0) return;
+    const int64_t ld = g.ld;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool mw = wave < MW;                      // matrix wave (else loader wave wave - MW)
+    const int lw = wave - MW;
+    const int lc = lane & 15, lk = lane >> 4;
+    unsigned long long touched = 0;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
+        __syncthreads();
+        const int64_t item = next_item;
+        if (item >= nitems) break;
+        const int64_t tile = item % ntiles, strip = item / ntiles;
+        const int64_t i0 = strip * rows;
+        const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
+        const int64_t c0 = tile * TW;
+        const int64_t cl = c0 + (mw ? wave * 16 : 0) + lc;          // a matrix lane's column
+        const bool in = mw && cl < g.ncols;
+        double b[G];
+        bool live = false;
+#pragma unroll
+        for (int gq = 0; gq < G; gq++) {
+            const int q = 4 * gq + lk;
+            const double v = (in && q < np) ? Pbuf[(int64_t)q * ld + cl] : 0.0;
+            b[gq] = -v;
+            live = live || v != 0.0;
+        }
+        live = (__shfl_xor((int)live, 16, 64) | (int)live) != 0;
+        live = (__shfl_xor((int)live, 32, 64) | (int)live) != 0;
+        const bool ok = in && (!skip || live);
+        int mine = (lk == 0 && ok) ? 1 : 0;
+        for (int mask = 32; mask > 0; mask >>= 1) mine += __shfl_xor(mine, mask, 64);
+        const bool wlive = mine > 0;                                   // wave-uniform
+        if (mw && lane == 0) wsum[wave] = mine;
+        if (__syncthreads_count(wlive && lane == 0) == 0) continue;    // the whole tile is skipped
+        if (threadIdx.x == 0) {
+            int sum = 0;
+#pragma unroll
+            for (int w = 0; w < MW; w++) sum += wsum[w];
+            touched += (unsigned long long)sum * (unsigned long long)(i1 - i0);
+        }
+        const int nb = (int)((i1 - i0 + 15) / 16);
+        // loader wave: band s into ring slot s % RING (rows past i1 and slots
+        // past np read the zero row; the tableau's last tile reads into the
+        // next row's padding, which the stores never write back)
+        auto issue = [&](int s) {
+            double *slot = ring + (size_t)(s % RING) * SLOT;
+#pragma unroll
+            for (int u = 0; u < TPW; u++) {
+                const int rr = lw * TPW + u;
+                const int64_t row = i0 + 16 * s + rr;
+                const double *src = row < i1 ? T + row * ld + c0 + 2 * lane : zrow + 2 * lane;
+                __builtin_amdgcn_global_load_lds((const void *)src, (void *)(slot + rr * TW), 16, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < CPW; u++) {
+                const int e = lw * CPW + u;                 // 8 slots x 16 rows per instruction
+                const int q = 8 * e + (lane >> 3);
+                const int64_t row = i0 + 16 * s + 2 * (lane & 7);
+                const double *src = (q < np && row < i1) ? Cbuf + (int64_t)q * cs + row : zrow + 2 * lane;
+                __builtin_amdgcn_global_load_lds((const void *)src, (void *)(slot + TB + e * 128), 16, 0, 0);
+            }
+        };
+        if (!mw && MODE != 2)
+            for (int s = 0; s < DT && s < nb; s++) issue(s);
+        for (int s = 0; s < nb; s++) {
+            if (!mw) {   // band s has landed (bands s+1 .. s+DT-1 may still be in flight)
+                if (s + DT - 1 < nb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DT - 1) * (TPW + CPW)) : "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            // band s is in the ring; slot (s - 1) % RING is free. A bare
+            // s_barrier: __syncthreads() would also wait for every wave's
+            // outstanding memory operations (vmcnt(0)), i.e. drain the DMA
+            // ring and the matrix waves' stores each band
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (!mw) {
+                if (MODE != 2 && s + DT < nb) issue(s + DT);
+            } else if (wlive) {
+                const double *slot = ring + (size_t)(s % RING) * SLOT;
+                d4 acc;
+#pragma unroll
+                for (int r = 0; r < 4; r++) acc[r] = slot[(lk + 4 * r) * TW + wave * 16 + lc];
+                const double *sa = slot + TB + lk * 16 + lc;
+#pragma unroll
+                for (int gq = 0; gq < G; gq++) if (MODE != 1) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[gq * 64], b[gq], acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int64_t row = i0 + 16 * s + lk + 4 * r;
+                    if (ok && row < i1) __builtin_nontemporal_store(acc[r], T + row * ld + cl);
+                }
+            }
+        }
+    }
+    if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
+}
+
+
 }  // namespace lpg
 
 using namespace lpg;
@@ -383,6 +894,58 @@ static void fn_w(Lab &L) {
     L.reset_state(L.K);
     hipLaunchKernelGGL((k_flushw<KMAX, NB, LB, 4>), dim3((unsigned)std::min<int64_t>(nitems, 256 * LB)), dim3(256), 0,
                        0, L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, (int64_t)R, 1);
+}
+
+template <int KMAX, int NB, int WPB, int R>
+static void fn_v(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 16 * WPB - 1) / (16 * WPB);
+    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
+    L.reset_state(L.K);
+    hipLaunchKernelGGL((k_flushv<KMAX, NB, WPB>), dim3((unsigned)std::min<int64_t>(nitems, 256)), dim3(64 * WPB), 0,
+                       0, L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, (int64_t)R, 1);
+}
+
+template <int KMAX, int NB, int WPB, int R, int MODE>
+static void fn_vp(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 16 * WPB - 1) / (16 * WPB);
+    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
+    L.reset_state(L.K);
+    hipLaunchKernelGGL((k_flushv_probe<KMAX, NB, WPB, MODE>), dim3((unsigned)std::min<int64_t>(nitems, 256)),
+                       dim3(64 * WPB), 0, 0, L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, (int64_t)R, 1);
+}
+
+template <int KMAX, int MW, int LW, int DT, int R>
+static void fn_s(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 16 * MW - 1) / (16 * MW);
+    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
+    const size_t lds = (size_t)(DT + 1) * (16 * 16 * MW + 16 * KMAX) * 8;
+    static bool set = false;
+    if (!set) {
+        CHK(hipFuncSetAttribute((const void *)k_flushs<KMAX, MW, LW, DT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+        set = true;
+    }
+    L.reset_state(L.K);
+    hipLaunchKernelGGL((k_flushs<KMAX, MW, LW, DT>), dim3((unsigned)std::min<int64_t>(nitems, 256)),
+                       dim3(64 * (MW + LW)), lds, 0, L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems,
+                       (int64_t)R, 1, (const double *)L.zbuf);
+}
+
+template <int KMAX, int MW, int LW, int DT, int R, int MODE>
+static void fn_sp(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 16 * MW - 1) / (16 * MW);
+    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
+    const size_t lds = (size_t)(DT + 1) * (16 * 16 * MW + 16 * KMAX) * 8;
+    static bool set = false;
+    if (!set) {
+        CHK(hipFuncSetAttribute((const void *)k_flushs_probe<KMAX, MW, LW, DT, MODE>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        set = true;
+    }
+    L.reset_state(L.K);
+    hipLaunchKernelGGL((k_flushs_probe<KMAX, MW, LW, DT, MODE>), dim3((unsigned)std::min<int64_t>(nitems, 256)),
+                       dim3(64 * (MW + LW)), lds, 0, L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems,
+                       (int64_t)R, 1, (const double *)L.zbuf);
 }
 
 template <int KMAX, int SB, int LB, int R>
@@ -484,9 +1047,21 @@ int main(int argc, char **argv) {
 #define X(KM, SB, LB, R) \
     if (want("x<" #KM "," #SB "," #LB "," #R ">")) run(L, fn_x<KM, SB, LB, R>, "x<" #KM "," #SB "," #LB "," #R ">", reps);
     W(128, 2, 1, 512)
+#define S(KM, MW, LW, DT, R) \
+    if (want("s<" #KM "," #MW "," #LW "," #DT "," #R ">")) run(L, fn_s<KM, MW, LW, DT, R>, "s<" #KM "," #MW "," #LW "," #DT "," #R ">", reps);
+    S(128, 8, 4, 3, 512)
+    S(128, 8, 4, 2, 512)
+    S(128, 8, 4, 3, 1024)
+    S(128, 8, 2, 3, 512)
+    S(128, 8, 8, 3, 512)
+#define V(KM, NB, WPB, R) \
+    if (want("v<" #KM "," #NB "," #WPB "," #R ">")) run(L, fn_v<KM, NB, WPB, R>, "v<" #KM "," #NB "," #WPB "," #R ">", reps);
+    V(128, 2, 8, 512)
+    V(128, 2, 8, 256)
+    V(128, 3, 8, 512)
+    V(128, 2, 16, 512)
+    V(128, 2, 4, 512)
     W(128, 3, 1, 512)
-    W(128, 4, 1, 512)
-    W(128, 3, 1, 1024)
     X(128, 2, 1, 512)
 #define Y(KM, LB, PF, R) \
     if (want("y<" #KM "," #LB "," #PF "," #R ">")) run(L, fn_y<KM, LB, PF, R>, "y<" #KM "," #LB "," #PF "," #R ">", reps);
@@ -494,5 +1069,12 @@ int main(int argc, char **argv) {
     g_nocheck = true;   // timing-only probes: no MFMA (memory alone), no tableau traffic (matrix cores alone)
     if (want("ymem")) run(L, fn_y<128, 1, 1, 2048, 1>, "ymem<128> (no MFMA)", reps);
     if (want("ymfma")) run(L, fn_y<128, 1, 1, 2048, 2>, "ymfma<128> (no T traffic)", reps);
+    if (want("sp")) run(L, fn_sp<128, 8, 4, 3, 1024, 1>, "sp1 (no MFMA)", reps);
+    if (want("sp")) run(L, fn_sp<128, 8, 4, 3, 1024, 2>, "sp2 (no DMA)", reps);
+    if (want("vp")) run(L, fn_vp<128, 2, 16, 512, 1>, "vp1 (no C staging)", reps);
+    if (want("vp")) run(L, fn_vp<128, 2, 16, 512, 2>, "vp2 (no T traffic)", reps);
+    if (want("vp")) run(L, fn_vp<128, 2, 16, 512, 3>, "vp3 (no band barrier)", reps);
+    if (want("vp")) run(L, fn_vp<128, 2, 8, 512, 1>, "vp1 w8 (no C staging)", reps);
+    if (want("vp")) run(L, fn_vp<128, 2, 8, 512, 2>, "vp2 w8 (no T traffic)", reps);
     return 0;
 }
