@@ -1,6 +1,7 @@
-"""Turn tools/profile.sh's rocprofv3 output (gpurun_out/prof) into committed evidence.
+"""Turn the rocprofv3 output of tools/gpu.sh's prof / pmc steps into committed evidence.
 
-  python tools/summarize_profile.py ROUND [CONFIG]
+  gpurun -- bash tools/gpu.sh "prof:rNN:ARGS" "pmc:rNN_fetch:FETCH_SIZE:ARGS" "pmc:rNN_write:WRITE_SIZE:ARGS"
+  python tools/summarize_profile.py ROUND [CONFIG]      (reads gpurun_out/prof_rNN, pmc_rNN_fetch, pmc_rNN_write)
 
 writes
   profiles/rNN_kernel_stats.csv     rocprofv3 --kernel-trace --stats summary (as produced)
@@ -23,11 +24,11 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PROF = os.path.join(ROOT, "gpurun_out", "prof")
+OUT = os.path.join(ROOT, "gpurun_out")
 
 
-def _one(pattern):
-    hits = sorted(glob.glob(os.path.join(PROF, "**", pattern), recursive=True))
+def _one(d, pattern):
+    hits = sorted(glob.glob(os.path.join(OUT, d, "**", pattern), recursive=True))
     return hits[0] if hits else None
 
 
@@ -52,7 +53,7 @@ def main():
     rnd = int(sys.argv[1])
     cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    stats = _one(os.path.join("trace", "**", "*kernel_stats.csv"))
+    stats = _one(f"prof_r{rnd:02d}", "*kernel_stats.csv")
     if stats:
         shutil.copy(stats, os.path.join(ROOT, "profiles", f"r{rnd:02d}_kernel_stats.csv"))
         with open(stats) as f:
@@ -60,8 +61,8 @@ def main():
         for r in rows:
             print(f"{short(r['Name']):>16s} calls={r['Calls']:>6s} avg_us={float(r['AverageNs']) / 1e3:10.2f} "
                   f"pct={float(r['Percentage']):6.2f}")
-    fetch = _one(os.path.join("fetch", "**", "*counter_collection.csv"))
-    write = _one(os.path.join("write", "**", "*counter_collection.csv"))
+    fetch = _one(f"pmc_r{rnd:02d}_fetch", "*counter_collection.csv")
+    write = _one(f"pmc_r{rnd:02d}_write", "*counter_collection.csv")
     out = {"config": cfg, "units": "KB per dispatch (rocprofv3 FETCH_SIZE / WRITE_SIZE)",
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts half "
                          "of a 16-B/lane streaming read; MI355X_MICROARCH.md §HBM)"}
@@ -92,8 +93,8 @@ def main():
         with open(os.path.join(ROOT, "profiles", f"pmc_config{cfg}.json"), "w") as f:
             json.dump({"hbm_bytes_per_launch": upd, "source": f"profiles/r{rnd:02d}_pmc.json",
                        "kernel": kern, "pending_pivots": pending, "fetch_factor": ff,
-                       "how": "tools/profile.sh: separate rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of "
-                              "bench.py (whole 64-pivot blocks, no warm-up), means over the block passes"}, f, indent=1)
+                       "how": "tools/gpu.sh pmc steps: separate rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes "
+                              "of bench.py (whole 64-pivot blocks, no warm-up), means over the block passes"}, f, indent=1)
     print(json.dumps(out, indent=1))
 
 
