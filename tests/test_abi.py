@@ -75,3 +75,22 @@ def test_errors_without_a_device_are_reported_not_raised():
     assert b"bad shape" in lib.lpg_last_error(None)
     rc = lib.lpg_create(ctypes.byref(ctx), 0, 0, 20, 0)                # m = 0
     assert rc == _lib.ERR_ARG
+
+
+def test_no_store_data_hazard_in_the_device_code():
+    """No >8-byte VMEM store in liblpg.so's gfx950 code has its data VGPRs
+    rewritten by VALU within two wait states (tools/store_hazard_scan.py:
+    hipcc emits that sequence after raw buffer stores, and with other waves
+    issuing on the SIMD the store then writes the new register values --
+    profiles/r03_overlap_lab.log)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import store_hazard_scan
+    finally:
+        sys.path.pop(0)
+    if not os.path.exists(store_hazard_scan.OBJDUMP):
+        pytest.skip("llvm-objdump not installed")
+    assert os.path.exists(LIB), "build first: make (or __graft_entry__.build())"
+    hits = store_hazard_scan.scan(LIB)
+    assert not hits, hits[:5]
