@@ -6,7 +6,7 @@ the device (splitmix64, seed 20220518). Each simplex pivot is price (argmin
 over the reduced-cost row) -> ratio test (min over the entering column) ->
 Gauss-Jordan rank-1 update of the whole tableau. The update is deferred:
 prep / select evaluate the pending chain for the entries they need and
-k_flushw applies each block of K pivots (LPG_DEFER; 128 for tableaus >= 16 GB
+k_flushw applies each block of K pivots (LPG_DEFER; 96 for tableaus >= 16 GB
 per rank, 64 from 200 MB, else 32) to the constraint rows in one HBM pass,
 bitwise identical to K eager updates.
 

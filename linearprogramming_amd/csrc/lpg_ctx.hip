@@ -439,7 +439,7 @@ static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
 }
 
 static constexpr int kGraphPivots = 32;
-static constexpr int kDefaultDeferHuge = 128;   // pivots per flush (LPG_DEFER), tableaus >= 16 GB per rank
+static constexpr int kDefaultDeferHuge = 96;    // pivots per flush (LPG_DEFER), tableaus >= 16 GB per rank
 static constexpr int kDefaultDefer = 64;        // pivots per flush, large tableaus
 static constexpr int kDefaultDeferSmall = 32;   // tableaus below 200 MB per rank
 
@@ -831,9 +831,11 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     // at 32, 99k at 64; m = 4096, n = 8192 (403 MB) 77k / 82k,
     // profiles/r02_k32_64.log)
     const int64_t nloc_guess = m * (rank + 1) / world - m * rank / world;
-    // 128 once it is >= 16 GB (too big for the persistent pivot kernel's
-    // slices; the 128-pivot pass is ~10% cheaper per pivot than two 64-pivot
-    // passes, tools/flush_lab.hip)
+    // 96 once it is >= 16 GB (too big for the persistent pivot kernel's
+    // slices, so the pair runs the pivots): the 96- and 128-pivot passes both
+    // sit at ~47 TFLOP/s on the matrix cores (the same cost per pivot, 23%
+    // below 64-pivot passes), and the pair's chains are shorter at 96 --
+    // config 4: 2,424 vs 2,347 pivots/s (profiles/r03_bench_config4_k96.json)
     const double tbytes = (double)nloc_guess * (double)ncols * 8.0;
     const int kdef = tbytes >= 16e9 ? kDefaultDeferHuge : tbytes >= 200e6 ? kDefaultDefer : kDefaultDeferSmall;
     c->defer_k = (flags & LPG_FLAG_EAGER) ? 0 : (dk ? atoi(dk) : kdef);

@@ -2305,6 +2305,7 @@ int flush_kmax_supported(int k) {
     if (k <= 16) return 16;
     if (k <= 32) return 32;
     if (k <= 64) return 64;
+    if (k <= 96) return 96;
     if (k <= 128 && k <= LPG_DEFER_MAX) return 128;
     return 0;
 }
@@ -2360,11 +2361,14 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
         int64_t rows = 512;
         while (rows > 64 && ntiles * ((g.nloc + rows - 1) / rows) < 2048) rows /= 2;
         const int64_t nitems = ntiles * ((g.nloc + rows - 1) / rows);
-        const int lb = kmax == 128 ? 1 : kmax == 64 ? 2 : 3;   // VGPRs: 184 at 64 slots, <= 128 below
+        const int lb = kmax == 128 ? 1 : kmax == 96 ? 2 : kmax == 64 ? 2 : 3;   // VGPRs: 184 at 64 slots, <= 128 below
         const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * lb);
         if (nblocks < 1) return 0;
         if (kmax == 128)
             hipLaunchKernelGGL((k_flushw<128, 2, 1, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
+                               D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
+        else if (kmax == 96)
+            hipLaunchKernelGGL((k_flushw<96, 2, 2, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
                                D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
         else if (kmax == 64)
             hipLaunchKernelGGL((k_flushw<64, 2, 2, kW64>), dim3((unsigned)((nblocks + 1) / 2)), dim3(64 * kW64), 0, stream,

@@ -110,7 +110,7 @@ def test_enqueue_past_optimal_partial_block(lpg, monkeypatch):
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("kernel,k", [("m", 8), ("m", 16), ("m", 32), ("w", 8), ("w", 32), ("w", 64), ("w", 128)])
+@pytest.mark.parametrize("kernel,k", [("m", 8), ("m", 16), ("m", 32), ("w", 8), ("w", 32), ("w", 64), ("w", 96), ("w", 128)])
 def test_flush_kernels_identical(lpg, monkeypatch, kernel, k):
     """k_flushm and k_flushw at their block sizes (LPG_FLUSH_KERNEL forces one)."""
     monkeypatch.setenv("LPG_FLUSH_KERNEL", kernel)
@@ -157,7 +157,7 @@ def test_bad_block_size(lpg, monkeypatch):
         lpg.Engine(8, 20)
 
 
-@pytest.mark.parametrize("kernel,k", [("m", 3), ("m", 8), ("m", 32), ("w", 3), ("w", 32), ("w", 64), ("w", 77), ("w", 128)])
+@pytest.mark.parametrize("kernel,k", [("m", 3), ("m", 8), ("m", 32), ("w", 3), ("w", 32), ("w", 64), ("w", 77), ("w", 96), ("w", 100), ("w", 128)])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1)])
 def test_flush_kernels_block_sizes(lpg, monkeypatch, kernel, k, m, n, seed, kind, rule):
     """k_flushm (strip-staged C) and k_flushw (tall banded items) at every

@@ -19,7 +19,7 @@ process per GPU), at the full sizes:
     lpg_info.residency_fallbacks counts it -- instead of waiting 2 s and
     failing (round 2).
 * config 4's shape (65536 x 131072, 32768 rows and 51.5 GB per rank, blocks
-  of 128 pivots, the multi-rank column trade over 196,609 columns), 320
+  of 96 pivots, the multi-rank column trade over 196,609 columns), 320
   pivots over the collectives (the owner push's spinning prep grid needs a GPU
   per rank at this size, see the test): bitwise equal to the single-rank engine (partition invariance: log,
   basis, objective row, column 0, every pivot row and 64 sampled rows per
@@ -159,10 +159,10 @@ def test_config4_shape_two_processes_partition_invariance(lpg):
     # spinning grid can hold every slot the owner's grid needs (one process per
     # GPU, the real layout, has no such coupling); config 3's 97-block grids fit
     parts = _run(2, m, n, piv, {}, push=False)
-    assert all(p["defer"] == 128 and p["wg"] == 0 and p["exchange"] == 0 for p in parts)   # the pair, 128-pivot blocks
+    assert all(p["defer"] == 96 and p["wg"] == 0 and p["exchange"] == 0 for p in parts)   # the pair, 96-pivot blocks
     # the same LP on one rank (run after the two processes have freed the GPU)
     e = lpg.Engine(m, n + m + 1)
-    assert e.info.defer_k == 128
+    assert e.info.defer_k == 96
     e.generate(n, SEED, lpg.GEN_DENSE)
     e.reserve_log(piv + 8)
     res = e.solve(piv, lpg.RULE_DANTZIG)

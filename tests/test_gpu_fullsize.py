@@ -9,8 +9,8 @@
 * config 5 (two-phase, Bland, m = n = 8192, KM-style degenerate with
   equality rows): the whole solve to optimality, bitwise against the oracle
   (status, pivot count, objective, log, basis, sampled rows).
-* config 4 (65536 x 131072, 103 GB tableau, one GPU): 320 pivots (two
-  whole 128-pivot blocks, then a partial one of 64); the oracle cannot hold it, so size-independent properties over the
+* config 4 (65536 x 131072, 103 GB tableau, one GPU): 320 pivots (three
+  whole 96-pivot blocks, then a partial one of 32); the oracle cannot hold it, so size-independent properties over the
   WHOLE tableau, read back in row chunks: every basic column is a unit vector
   in every row, b >= 0 (primal feasibility), z is nondecreasing block to block,
   and the objective row equals c_B T - c (recomputed on the host in global row
@@ -108,13 +108,13 @@ def test_config4_full_size_properties(lpg):
     m, n = 65536, 131072
     N1 = n + m + 1
     e = lpg.Engine(m, N1)
-    assert e.info.defer_k == 128                 # >= 16 GB: 128-pivot blocks
+    assert e.info.defer_k == 96                  # >= 16 GB: 96-pivot blocks
     e.generate(n, SEED, lpg.GEN_DENSE)
     c = -e.get_rows(m, 1)[0, 1:]                # slack basis: row m = [0 | -c]
     assert np.all(c[:n] > 0) and np.all(c[n:] == 0)
     e.reserve_log(512)
     zs = [0.0]
-    for step in (128, 128, 64):
+    for step in (96, 96, 96, 32):
         r = e.solve(step, lpg.RULE_DANTZIG)
         assert r.status_name == "ITER_LIMIT"
         zs.append(r.objective)

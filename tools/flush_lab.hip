@@ -830,6 +830,116 @@ __global__ __launch_bounds__(64 * (MW + LW)) void k_flushs_probe(double *__restr
 }
 
 
+// k_flushg (round 3): no LDS and no barrier. Each WAVE takes its own items
+// (32-column tile x `rows` rows) from the queue; B = P in VGPRs for the item,
+// A = -C straight from the Infinity Cache / L2 by buffer loads (one VGPR
+// offset, the slot stride in an SGPR), A of band s+1 loaded into the register
+// its band-s MFMA just read, tableau bands DEP ahead. Same chain as k_flushw
+// (slots in ascending order, A = -C, B = P; past np A = -0, B = +0), so the
+// results are bitwise. Every 16-byte store is followed by s_nop 1: hipcc
+// emits none after raw buffer stores, and a VALU write of the store's data
+// registers right behind it corrupts the stored value when other waves share
+// the SIMD (tools/overlap_lab.hip, tools/store_hazard_scan.py).
+template <int KMAX, int DEP, int LB>
+__global__ __launch_bounds__(256, LB) void k_flushg(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+                                                    const double *__restrict__ Pbuf, const double *__restrict__ Cbuf,
+                                                    int64_t cs, int64_t ntiles, int64_t nitems, int64_t rows,
+                                                    int skip) {
+    constexpr int G = KMAX / 4;
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+    const int np = (int)st->npend;
+    if (np <= 0) return;
+    const int64_t ld = g.ld;
+    const int lane = threadIdx.x & 63;
+    const int lc = lane & 15, lk = lane >> 4;
+    unsigned long long touched = 0;
+    const __amdgpu_buffer_rsrc_t rc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Cbuf), (short)0, (int)(KMAX * cs * 8), 0x00020000);
+    for (;;) {
+        int64_t item = 0;
+        if (lane == 0) item = (int64_t)atomicAdd(&st->fwork, 1ull);
+        item = (int64_t)__builtin_amdgcn_readfirstlane((int)item);
+        if (item >= nitems) break;
+        const int64_t tile = item % ntiles, strip = item / ntiles;
+        const int64_t i0 = strip * rows;
+        const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
+        const int64_t cl = tile * 32 + 2 * lc;
+        const bool in = cl < g.ncols;
+        double be[G], bo[G];
+        bool live = false;
+#pragma unroll
+        for (int gq = 0; gq < G; gq++) {
+            const int q = 4 * gq + lk;
+            d2 v = d2{0.0, 0.0};
+            if (in && q < np) v = *(const d2 *)(Pbuf + (int64_t)q * ld + cl);
+            be[gq] = v.x;
+            bo[gq] = v.y;
+            live = live || v.x != 0.0 || v.y != 0.0;
+        }
+        live = (__shfl_xor((int)live, 16, 64) | (int)live) != 0;
+        live = (__shfl_xor((int)live, 32, 64) | (int)live) != 0;
+        const bool ok = in && (!skip || live);
+        int mine = (lk == 0 && ok) ? (cl + 1 < g.ncols ? 2 : 1) : 0;
+        for (int mask = 32; mask > 0; mask >>= 1) mine += __shfl_xor(mine, mask, 64);
+        if (mine == 0) continue;                        // wave-uniform: the whole tile is skipped
+        if (lane == 0) touched += (unsigned long long)mine * (unsigned long long)(i1 - i0);
+        const int nb = (int)((i1 - i0 + 15) / 16);
+        const int voffT = (int)(((int64_t)lk * ld + cl) * 8);
+        const int voffA = (int)(((int64_t)lk * cs + i0 + lc) * 8);
+        auto band_rsrc = [&](int s) {
+            return __builtin_amdgcn_make_buffer_rsrc(T + (i0 + (int64_t)16 * s) * ld, (short)0, (int)(16 * ld * 8),
+                                                     0x00020000);
+        };
+        auto tload = [&](d2 (&x)[4], int s) {
+            const __amdgpu_buffer_rsrc_t rt = band_rsrc(s);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const bool v = ok && i0 + 16 * s + lk + 4 * r < i1;
+                const u4v w = __builtin_amdgcn_raw_buffer_load_b128(rt, voffT, (int)(r * 4 * ld * 8), 2);
+                x[r] = v ? __builtin_bit_cast(d2, w) : d2{0.0, 0.0};
+            }
+        };
+        auto aload1 = [&](int s, int gq) -> double {
+            const bool v = s < nb && 4 * gq + lk < np && i0 + 16 * s + lc < i1;
+            const auto w = __builtin_amdgcn_raw_buffer_load_b64(rc, voffA + s * 16 * 8, (int)(gq * 4 * cs * 8), 0);
+            return v ? -__builtin_bit_cast(double, w) : -0.0;
+        };
+        double a[G];
+#pragma unroll
+        for (int gq = 0; gq < G; gq++) a[gq] = aload1(0, gq);
+        d2 tb[DEP][4];
+#pragma unroll
+        for (int d = 0; d < DEP; d++) tload(tb[d], d);
+        for (int s0 = 0; s0 < nb; s0 += DEP) {
+#pragma unroll
+            for (int d = 0; d < DEP; d++) {
+                const int s = s0 + d;
+                if (s < nb) {
+                    d4 ae = d4{tb[d][0].x, tb[d][1].x, tb[d][2].x, tb[d][3].x};
+                    d4 ao = d4{tb[d][0].y, tb[d][1].y, tb[d][2].y, tb[d][3].y};
+#pragma unroll
+                    for (int gq = 0; gq < G; gq++) {
+                        ae = __builtin_amdgcn_mfma_f64_16x16x4f64(a[gq], be[gq], ae, 0, 0, 0);
+                        ao = __builtin_amdgcn_mfma_f64_16x16x4f64(a[gq], bo[gq], ao, 0, 0, 0);
+                        a[gq] = aload1(s + 1, gq);
+                    }
+                    const __amdgpu_buffer_rsrc_t rt = band_rsrc(s);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        if (ok && i0 + 16 * s + lk + 4 * r < i1)
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d2{ae[r], ao[r]}), rt, voffT,
+                                                                   (int)(r * 4 * ld * 8), 2);
+                        asm volatile("s_nop 1" ::: "memory");
+                    }
+                    if (s + DEP < nb) tload(tb[d], s + DEP);
+                }
+            }
+        }
+    }
+    if (lane == 0 && touched) atomicAdd(&st->touched, touched);
+}
+
+
 }  // namespace lpg
 
 using namespace lpg;
@@ -966,6 +1076,25 @@ static void fn_y(Lab &L) {
                        L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, (int64_t)R, 1);
 }
 
+
+template <int KMAX, int DEP, int LB, int R>
+static void fn_g(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 31) / 32;
+    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
+    L.reset_state(L.K);
+    hipLaunchKernelGGL((k_flushg<KMAX, DEP, LB>), dim3(256 * LB), dim3(256), 0, 0, L.g.T, L.g, L.st, L.Pbuf, L.Cbuf,
+                       L.cs, ntiles, nitems, (int64_t)R, 1);
+}
+
+// 96-slot reference: the product's k_flushw<96> (bitwise = the fma chain, tests/test_gpu_defer.py)
+static void fn_ref96(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 127) / 128, rows = 512;
+    const int64_t nitems = ntiles * ((L.g.nloc + rows - 1) / rows);
+    L.reset_state(96);
+    hipLaunchKernelGGL((k_flushw<96, 2, 2, 4>), dim3((unsigned)std::min<int64_t>(nitems, 512)), dim3(256), 0, 0, L.g.T,
+                       L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, rows, 1);
+}
+
 static bool g_nocheck = false;
 static double run(Lab &L, LaunchFn fn, const char *name, int reps) {
     CHK(hipMemcpy(L.T, L.T0, L.n * 8, hipMemcpyDeviceToDevice));
@@ -1034,7 +1163,22 @@ int main(int argc, char **argv) {
     CHK(hipEventCreate(&L.e1));
     printf("flush lab: %lld rows x %lld cols (ld %lld), K=%d, P zero for columns > %lld\n", (long long)m,
            (long long)ncols, (long long)ld, L.K, (long long)nstruct);
+    if (getenv("LAB_K")) L.K = atoi(getenv("LAB_K"));
     CHK(hipMemcpy(L.T, L.T0, L.n * 8, hipMemcpyDeviceToDevice));
+    if (L.K == 96) {   // k_flushw<96> is the reference; then the global-A form against it, and stop
+        fn_ref96(L);
+        CHK(hipDeviceSynchronize());
+        CHK(hipMemcpy(L.Tref, L.T, L.n * 8, hipMemcpyDeviceToDevice));
+        run(L, fn_ref96, "w<96,2,2,512> (product)", 5);
+        run(L, fn_g<96, 2, 1, 512>, "g<96,dep2,1 wave/SIMD,512>", 5);
+        run(L, fn_g<96, 2, 2, 512>, "g<96,dep2,2 waves/SIMD,512>", 5);
+        run(L, fn_g<96, 3, 1, 512>, "g<96,dep3,1 wave/SIMD,512>", 5);
+        run(L, fn_g<96, 1, 2, 512>, "g<96,dep1,2 waves/SIMD,512>", 5);
+        run(L, fn_g<96, 2, 2, 1024>, "g<96,dep2,2 waves/SIMD,1024>", 5);
+        run(L, fn_g<96, 2, 2, 256>, "g<96,dep2,2 waves/SIMD,256>", 5);
+        run(L, fn_ref96, "w<96,2,2,512> (product)", 5);
+        return 0;
+    }
     fn_ref(L);
     CHK(hipDeviceSynchronize());
     CHK(hipMemcpy(L.Tref, L.T, L.n * 8, hipMemcpyDeviceToDevice));
