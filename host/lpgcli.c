@@ -7,7 +7,7 @@
  * reference's own language: it builds or reads a tableau, calls the C-ABI and
  * prints one JSON line, so nothing blocks on stdin.
  *
- *   lpgcli --synthetic M N [--seed S] [--kind dense|degenerate]
+ *   lpgcli --synthetic M N [--seed S] [--kind dense|degenerate|artificial]
  *          [--rule dantzig|bland] [--pivots K] [--device D]
  *   lpgcli --tableau FILE [--rule ...] [--pivots K]
  *   lpgcli --lp MODEL [--big-m] [--rule ...]     the reference's model format,
@@ -17,7 +17,10 @@
  *          reference leaves empty): with --lp, LPStandardize's dual form
  *          (simplex.c:178-179) solved from its slack basis; with --synthetic,
  *          the dual-feasible LPG_GEN_DUAL tableau; with --tableau, the file's
- *          (dual-feasible) basis. Single rank.
+ *          (dual-feasible) basis; also over --gpus P (round 3).
+ *   --kind artificial  BASELINE config 5's family (equality rows with
+ *          artificial unit columns) solved by the two-phase method
+ *          (lpg_solve_two_phase), on one rank or over --gpus P (round 3).
  *   lpgcli --synthetic M N --gpus P [--exchange push|host]
  *          the row partition over P ranks, one process each (forked before
  *          any HIP call; the parent only relays the host-staged collectives
@@ -55,11 +58,12 @@ static const char *status_name(int s) {
 }
 
 static int usage(const char *argv0) {
-    fprintf(stderr, "Usage:\n\t%s --synthetic M N [--seed S] [--kind dense|degenerate] [--rule dantzig|bland]"
+    fprintf(stderr, "Usage:\n\t%s --synthetic M N [--seed S] [--kind dense|degenerate|artificial] [--rule dantzig|bland]"
                     " [--pivots K] [--device D] [--gpus P [--exchange push|host]]\n"
                     "\t%s --tableau FILE [--rule dantzig|bland] [--pivots K]\n"
                     "\t%s --lp MODEL [--big-m | --dual] [--rule dantzig|bland]\n\t%s --lp-dump MODEL [--dual]\n"
-                    "\t(--dual: the dual simplex; also with --synthetic and --tableau, single rank)\n",
+                    "\t(--dual: the dual simplex; also with --synthetic (any --gpus) and --tableau;\n"
+                    "\t --kind artificial: the two-phase method)\n",
             argv0, argv0, argv0, argv0);
     return 2;
 }
@@ -195,8 +199,22 @@ done:
 typedef struct {
     long long m, n, pivots;
     unsigned long long seed;
-    int kind, rule, device, world, push;
+    int kind, rule, device, world, push, dual;
 } dist_args;
+
+/* the solve a synthetic tableau asks for: the dual on LPG_GEN_DUAL, the
+ * two-phase method on LPG_GEN_ARTIFICIAL (its artificial columns start at
+ * 1 + n + ceil(m / 2), as lpg_generate lays them out), else the primal */
+static int solve_synthetic(lpg_ctx *ctx, long long m, long long n, int kind, int dual, long long pivots, int rule,
+                           lpg_result *res) {
+    if (dual) return lpg_solve_dual(ctx, pivots, res);
+    if (kind == LPG_GEN_ARTIFICIAL) return lpg_solve_two_phase(ctx, 1 + n + (m + 1) / 2, NULL, pivots, rule, res);
+    return lpg_solve(ctx, pivots, rule, res);
+}
+
+static const char *method_name(int kind, int dual) {
+    return dual ? "dual" : kind == LPG_GEN_ARTIFICIAL ? "two-phase" : "primal";
+}
 
 static int run_rank(const dist_args *a, int rank, int fd) {
     hub_link h = {fd, a->world, rank};
@@ -220,12 +238,12 @@ static int run_rank(const dist_args *a, int rank, int fd) {
         free(all);
         if (rc) goto fail;
     }
-    if ((rc = lpg_generate(ctx, a->n, a->seed, a->kind)) != 0) goto fail;
+    if ((rc = lpg_generate(ctx, a->n, a->seed, a->dual ? LPG_GEN_DUAL : a->kind)) != 0) goto fail;
     char one = 1, got[256];
     if (a->world > 256 || cb_allgather(&h, &one, got, 1)) goto fail;   /* start together */
     const double t0 = now();
     lpg_result res;
-    if ((rc = lpg_solve(ctx, a->pivots, a->rule, &res)) != 0) goto fail;
+    if ((rc = solve_synthetic(ctx, a->m, a->n, a->kind, a->dual, a->pivots, a->rule, &res)) != 0) goto fail;
     if (cb_allgather(&h, &one, got, 1)) goto fail;                     /* the slowest rank's end */
     const double dt = now() - t0;
     lpg_info_t info;
@@ -235,10 +253,11 @@ static int run_rank(const dist_args *a, int rank, int fd) {
         printf("{\"status\": \"%s\", \"pivots\": %lld, \"objective\": %.17g, \"seconds\": %.6f, "
                "\"pivots_per_s\": %.3f, \"m\": %lld, \"ncols\": %lld, \"rule\": \"%s\", \"gpus\": %d, "
                "\"exchange\": %d, \"pivot_wg\": %d, \"residency_fallbacks\": %d, \"defer_k\": %d, "
-               "\"log_fnv\": \"%016llx\"}\n",
+               "\"method\": \"%s\", \"log_fnv\": \"%016llx\"}\n",
                status_name(res.status), (long long)res.pivots, res.objective, dt, dt > 0 ? (double)res.pivots / dt : 0.0,
-               (long long)info.m, (long long)info.ncols, a->rule == LPG_RULE_BLAND ? "bland" : "dantzig", a->world,
-               info.exchange, info.pivot_wg, info.residency_fallbacks, info.defer_k, (unsigned long long)fnv);
+               (long long)info.m, (long long)info.ncols, a->rule == LPG_RULE_BLAND && !a->dual ? "bland" : "dantzig",
+               a->world, info.exchange, info.pivot_wg, info.residency_fallbacks, info.defer_k,
+               method_name(a->kind, a->dual), (unsigned long long)fnv);
     fflush(stdout);
     lpg_destroy(ctx);
     close(fd);
@@ -451,7 +470,9 @@ int main(int argc, char **argv) {
         } else if (!strcmp(argv[a], "--seed") && a + 1 < argc) {
             seed = strtoull(argv[++a], NULL, 10);
         } else if (!strcmp(argv[a], "--kind") && a + 1 < argc) {
-            kind = !strcmp(argv[++a], "degenerate") ? LPG_GEN_DEGENERATE : LPG_GEN_DENSE;
+            ++a;
+            kind = !strcmp(argv[a], "degenerate") ? LPG_GEN_DEGENERATE
+                   : !strcmp(argv[a], "artificial") ? LPG_GEN_ARTIFICIAL : LPG_GEN_DENSE;
         } else if (!strcmp(argv[a], "--rule") && a + 1 < argc) {
             rule = !strcmp(argv[++a], "bland") ? LPG_RULE_BLAND : LPG_RULE_DANTZIG;
         } else if (!strcmp(argv[a], "--pivots") && a + 1 < argc) {
@@ -466,11 +487,11 @@ int main(int argc, char **argv) {
             return usage(argv[0]);
         }
     }
-    if (dual && (bigm || gpus > 1)) return usage(argv[0]);
+    if (dual && (bigm || kind == LPG_GEN_ARTIFICIAL)) return usage(argv[0]);
     if (lpfile) return run_lp(lpfile, dump, dual ? LPF_DUAL : bigm ? LPF_BIG_M : LPF_TWO_PHASE, rule, device);
     if (gpus > 1) {
         if (!(m > 0 && n > 0) || gpus > m || gpus > 64) return usage(argv[0]);
-        const dist_args da = {m, n, pivots, seed, kind, rule, device, gpus, push};
+        const dist_args da = {m, n, pivots, seed, kind, rule, device, gpus, push, dual};
         return run_dist(&da);
     }
     lpg_ctx *ctx = NULL;
@@ -492,7 +513,8 @@ int main(int argc, char **argv) {
     }
     lpg_result res;
     const double t0 = now();
-    rc = dual ? lpg_solve_dual(ctx, pivots, &res) : lpg_solve(ctx, pivots, rule, &res);
+    rc = file ? (dual ? lpg_solve_dual(ctx, pivots, &res) : lpg_solve(ctx, pivots, rule, &res))
+              : solve_synthetic(ctx, m, n, kind, dual, pivots, rule, &res);
     const double dt = now() - t0;
     if (rc != 0) {
         fprintf(stderr, "ERROR: %s\n", lpg_last_error(ctx));
@@ -506,7 +528,7 @@ int main(int argc, char **argv) {
            "\"defer_k\": %d, \"method\": \"%s\", \"log_fnv\": \"%016llx\"}\n",
            status_name(res.status), (long long)res.pivots, res.objective, dt, dt > 0 ? (double)res.pivots / dt : 0.0,
            (long long)info.m, (long long)info.ncols, rule == LPG_RULE_BLAND && !dual ? "bland" : "dantzig", info.defer_k,
-           dual ? "dual" : "primal", (unsigned long long)log_fnv(ctx, res.pivots));
+           file ? (dual ? "dual" : "primal") : method_name(kind, dual), (unsigned long long)log_fnv(ctx, res.pivots));
     lpg_destroy(ctx);
     return 0;
 }

@@ -231,7 +231,8 @@ int  lpg_prepare(lpg_ctx *ctx, int rule);
 
 /* Apply one caller-chosen pivot (entering column k, 1-based; leaving row r,
  * 0-based) with the same arithmetic as the loop; |T[r][k]| must exceed
- * eps_piv (either sign). Counts as a pivot and is logged. */
+ * eps_piv (either sign). Counts as a pivot and is logged. On a row partition
+ * every rank calls it with the same (k, r). */
 int  lpg_pivot(lpg_ctx *ctx, int64_t k, int64_t r);
 /* Two-phase method for a tableau whose columns art_first..N are artificial
  * unit columns basic in the rows that lacked an identity column
@@ -241,7 +242,10 @@ int  lpg_pivot(lpg_ctx *ctx, int64_t k, int64_t r);
  * first usable original column of their row. Phase II prices columns
  * 1..art_first-1 only, with the objective row recomputed from cost[0..N-1]
  * (cost NULL: -1 x the objective row as loaded, i.e. a slack-form -c row).
- * Single rank. */
+ * On a row partition every rank calls it with the same arguments (it is
+ * collective): the |b| sum of the feasibility test runs over the ranks in
+ * global row order, and each artificial row's owner finds its column and
+ * shares it through the communicator before every rank pivots (round 3). */
 int  lpg_solve_two_phase(lpg_ctx *ctx, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
                          lpg_result *out);
 

@@ -55,6 +55,7 @@ struct lpg_ctx {
     Cand *part = nullptr;         // nsel (this rank's select partials)
     Cand *cand = nullptr;         // world * nsel (gathered); == part when world == 1
     Cand *drc = nullptr, *dcp = nullptr;   // deferred dual: row candidates, ratio-test partials (lazy)
+    Cand *drc_all = nullptr;               // ... every rank's row candidates (row partition)
     int64_t *basis = nullptr;     // m (replicated)
     int64_t *logk = nullptr, *logr = nullptr;
     int64_t logcap = 0;
@@ -1113,7 +1114,7 @@ void lpg_destroy(lpg_ctx *c) {
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
                     c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->mul, c->pv, c->tmp,
-                    c->rec, c->drc, c->dcp};
+                    c->rec, c->drc, c->dcp, c->drc_all};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -1361,16 +1362,50 @@ int lpg_pivot(lpg_ctx *c, int64_t k, int64_t r) {
     return 0;
 }
 
+// Sums of host values over ranks: count doubles through the device scratch
+// `acc` and the attached communicator (no-op on one rank).
+static int host_allreduce_sum(lpg_ctx *c, double *v, size_t count) {
+    if (!has_comm(c)) return 0;
+    if (count > (size_t)c->ncols) return fail(c, LPG_ERR_ARG, "host_allreduce_sum: %zu > ncols", count);
+    HIPCHK(c, hipMemcpyAsync(c->acc, v, count * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    int rc;
+    if ((rc = comm_allreduce_sum(c, c->acc, count))) return rc;
+    HIPCHK(c, hipMemcpyAsync(v, c->acc, count * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// sum |b_i| over every constraint row in global row order, the same double
+// on every rank: rank p continues rank p - 1's running sum (the others add
+// +0), so the rounding is the single rank's
+static int abs_b_sum(lpg_ctx *c, double *out) {
+    std::vector<double> xb(std::max<int64_t>(c->nloc, 1));
+    int rc;
+    if ((rc = lpg_get_column0(c, xb.data()))) return rc;
+    double s = 0.0;
+    for (int p = 0; p < c->world; p++) {
+        double v = 0.0;
+        if (p == c->rank) {
+            v = s;
+            for (int64_t i = 0; i < c->nloc; i++) v += fabs(xb[i]);
+        }
+        if (c->world > 1 && (rc = host_allreduce_sum(c, &v, 1))) return rc;
+        s = v;
+    }
+    *out = s;
+    return 0;
+}
+
 int lpg_solve_two_phase(lpg_ctx *c, int64_t art_first, const double *cost, int64_t max_pivots, int rule,
                         lpg_result *out) {
     if (!c || art_first < 2 || art_first >= c->ncols || max_pivots < 0)
         return fail(c, LPG_ERR_ARG, "lpg_solve_two_phase: bad arguments");
-    if (c->world != 1) return fail(c, LPG_ERR_STATE, "lpg_solve_two_phase: single rank only");
+    if (c->world > 1 && !has_comm(c)) return fail(c, LPG_ERR_STATE, "lpg_solve_two_phase: no communicator attached");
     int rc;
     if ((rc = use_device(c))) return rc;
     const int64_t N = c->ncols - 1;
     std::vector<double> own;
-    if (!cost) {   // costs = -1 x the objective row as loaded (slack-form -c row)
+    if (!cost) {   // costs = -1 x the objective row as loaded (slack-form -c row, replicated)
         own.resize(c->ncols);
         if ((rc = lpg_get_rows(c, c->m, 1, own.data(), c->ncols))) return rc;
         for (int64_t j = 1; j <= N; j++) own[j - 1] = -own[j];
@@ -1389,11 +1424,7 @@ int lpg_solve_two_phase(lpg_ctx *c, int64_t art_first, const double *cost, int64
     }
     // infeasible when the artificials cannot all reach zero
     double bsum = 0;
-    {
-        std::vector<double> xb(c->nloc);
-        if ((rc = lpg_get_column0(c, xb.data()))) return rc;
-        for (double v : xb) bsum += fabs(v);
-    }
+    if ((rc = abs_b_sum(c, &bsum))) return rc;
     if (r1.objective < -1e-9 * std::max(1.0, bsum)) {
         if (out) { *out = r1; out->status = LPG_INFEASIBLE; }
         return 0;
@@ -1401,18 +1432,27 @@ int lpg_solve_two_phase(lpg_ctx *c, int64_t art_first, const double *cost, int64
     // Drive artificials still basic (at zero) out of the basis with forced
     // degenerate pivots on the first usable original column of their row; a
     // row with no such column is redundant and keeps its artificial at zero.
+    // Row i lives on one rank: its owner finds the column and every rank
+    // learns it through a sum (the others add 0), then every rank pivots.
     std::vector<int64_t> basis(c->m);
     if ((rc = lpg_get_basis(c, basis.data()))) return rc;
     std::vector<double> row(c->ncols);
     for (int64_t i = 0; i < c->m; i++) {
         if (basis[i] < art_first) continue;
-        if ((rc = lpg_get_rows(c, i, 1, row.data(), c->ncols))) return rc;
-        for (int64_t j = 1; j < art_first; j++)
-            if (fabs(row[j]) > c->eps_piv) {
-                if ((rc = lpg_pivot(c, j, i))) return rc;
-                used++;
-                break;
-            }
+        double jv = 0.0;
+        if (i >= c->row0 && i < c->row0 + c->nloc) {
+            if ((rc = lpg_get_rows(c, i, 1, row.data(), c->ncols))) return rc;
+            for (int64_t j = 1; j < art_first; j++)
+                if (fabs(row[j]) > c->eps_piv) {
+                    jv = (double)j;
+                    break;
+                }
+        }
+        if (c->world > 1 && (rc = host_allreduce_sum(c, &jv, 1))) return rc;
+        if (jv > 0.0) {
+            if ((rc = lpg_pivot(c, (int64_t)jv, i))) return rc;
+            used++;
+        }
     }
     // Phase II: original costs, artificial columns barred from entering.
     if ((rc = lpg_set_active_columns(c, art_first - 1)) || (rc = lpg_set_objective(c, cost))) return rc;
@@ -1470,9 +1510,14 @@ int lpg_solve_big_m(lpg_ctx *c, int64_t art_first, const double *cost, int64_t m
 static int solve_dual_deferred(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
     const Geo g = geo(c);
     const Launch L = lau(c);
-    const int nrc = pivot_d_blocks(g, 1, 256), ncp = pivot_d_blocks(g, 0, 256);
+    const bool mr = has_comm(c);
+    // row-candidate blocks: the same count on every rank (the largest row block)
+    int64_t maxloc = 0;
+    for (int p = 0; p < c->world; p++) maxloc = std::max(maxloc, c->m * (p + 1) / c->world - c->m * p / c->world);
+    const int nrc = (int)((maxloc + c->nobj + 255) / 256), ncp = pivot_d_blocks(g, 0, 256);
     if (!c->drc) HIPCHK(c, hipMalloc(&c->drc, (size_t)nrc * sizeof(Cand)));
     if (!c->dcp) HIPCHK(c, hipMalloc(&c->dcp, (size_t)ncp * sizeof(Cand)));
+    if (mr && !c->drc_all) HIPCHK(c, hipMalloc(&c->drc_all, (size_t)nrc * c->world * sizeof(Cand)));
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
     if (launch_dual_rows(L, g, c->drc, nrc)) return fail(c, LPG_ERR_DEVICE, "dual rows launch failed");
     c->par = 0;
@@ -1480,20 +1525,32 @@ static int solve_dual_deferred(lpg_ctx *c, int64_t max_pivots, lpg_result *out) 
     const bool keep = c->no_reorder;
     c->no_reorder = true;
     int rc = 0;
-    auto pivot = [&](bool row_only) {
+    // one pivot: (MR: every rank's row candidates) row_d, (MR: R summed over
+    // the ranks, the ratio partials) col_d; row_only: row_d alone
+    auto pivot = [&](bool row_only) -> int {
         const int s = c->par;
         const Defer D = defer_of(c, c->pend);
         const double *Pprev = c->Pbuf + (int64_t)((c->pend + c->defer_k - 1) % c->defer_k) * c->ld;
-        return launch_dual_pivot_d(L, g, c->st, s, c->drc, nrc, c->dcp, ncp, c->P, Pprev, c->C[s ^ 1], c->C[s], D,
-                                   row_only);
+        int r2;
+        if (mr && (r2 = comm_allgather(c, c->drc, c->drc_all, (size_t)nrc * sizeof(Cand)))) return r2;
+        if (launch_dual_row_d(L, g, c->st, s, mr ? c->drc_all : c->drc, mr ? nrc * c->world : nrc, c->dcp, c->P,
+                              Pprev, c->C[s ^ 1], D, mr))
+            return fail(c, LPG_ERR_DEVICE, "dual row launch failed");
+        if (row_only) return 0;
+        if (mr) {
+            if ((r2 = comm_allreduce_sum(c, c->P, (size_t)prow_count(c)))) return r2;
+            if (launch_dual_ratio(L, g, c->st, s, c->P, c->dcp)) return fail(c, LPG_ERR_DEVICE, "dual ratio launch failed");
+        }
+        if (launch_dual_col_d(L, g, c->st, s, c->dcp, c->P, c->C[s], c->drc, nrc, D))
+            return fail(c, LPG_ERR_DEVICE, "dual column launch failed");
+        return 0;
     };
     int64_t done = 0, batch = 8;
     while (done < max_pivots) {
         const int64_t n = std::min(batch, max_pivots - done);
         if ((rc = ensure_log(c, c->enq + n))) break;
         for (int64_t q = 0; q < n && !rc; q++) {
-            if (pivot(false)) rc = fail(c, LPG_ERR_DEVICE, "dual pivot launch failed");
-            else if (++c->pend == c->defer_k) rc = flush_launch(c);
+            if (!(rc = pivot(false)) && ++c->pend == c->defer_k) rc = flush_launch(c);
             c->par ^= 1;
             c->enq++;
         }
@@ -1505,7 +1562,7 @@ static int solve_dual_deferred(lpg_ctx *c, int64_t max_pivots, lpg_result *out) 
         if (h.slot[c->par].status != LPG_RUNNING) break;
         batch = std::min<int64_t>(batch * 2, 256);
     }
-    if (!rc && pivot(true)) rc = fail(c, LPG_ERR_DEVICE, "dual row launch failed");
+    if (!rc) rc = pivot(true);
     if (!rc && hipMemsetAsync(&c->st->slot[c->par].dpend, 0, sizeof(int64_t), c->stream) != hipSuccess)
         rc = fail(c, LPG_ERR_DEVICE, "hipMemsetAsync failed");
     if (!rc) rc = materialize(c);
@@ -1530,7 +1587,9 @@ static int solve_dual_deferred(lpg_ctx *c, int64_t max_pivots, lpg_result *out) 
 
 int lpg_solve_dual(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
     if (!c || max_pivots < 0) return fail(c, LPG_ERR_ARG, "lpg_solve_dual: bad arguments");
-    if (c->world != 1 || has_comm(c)) return fail(c, LPG_ERR_STATE, "lpg_solve_dual: single rank only");
+    if (c->world > 1 && !has_comm(c)) return fail(c, LPG_ERR_STATE, "lpg_solve_dual: no communicator attached");
+    if (has_comm(c) && !(c->defer_k > 0 && c->nobj == 1))
+        return fail(c, LPG_ERR_STATE, "lpg_solve_dual: a row partition runs the deferred form only (not LPG_FLAG_EAGER)");
     int rc;
     if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;
     // the dual simplex starts from a dual-feasible basis: every d_j >= -eps

@@ -33,6 +33,14 @@
 // the eager update's fma(-C_t[obj], P_t[j], d_j), one kernel later. The slot's
 // `dpend` word carries "an objective update is owed" from col_d to the next
 // row_d (or to the host's final row_d, which also peeks at optimality).
+//
+// Row partition (MR, round 3): the row candidates row_d reduces are every
+// rank's (allgathered by the host); the owner of r_t writes row r_t into R and
+// every other rank -0, the host sums R over the ranks (the owner's row bit
+// for bit), and the ratio partials come from R and the replicated objective
+// row in k_dual_ratio, the same on every rank; col_d then runs on each rank's
+// rows with r_t's local index (-1 off the owner). P_t, the objective row, the
+// basis and the log are replicated; C_t and the flush are per rank.
 #include <hip/hip_runtime.h>
 
 #include "lpg_device.h"
@@ -61,7 +69,7 @@ __device__ __forceinline__ void ratio_cand(Cand &best, double a, double d, int64
     cand_take(best, c, cand_better(c, best));
 }
 
-template <int kPF>
+template <int kPF, bool MR>
 __global__ __launch_bounds__(256) void k_dual_row_d(double *__restrict__ T, Geo g, DevState *st, int s,
                                                     const Cand *__restrict__ rc, int nrc,
                                                     const double *__restrict__ Pprev, const double *__restrict__ Cprev,
@@ -93,7 +101,14 @@ __global__ __launch_bounds__(256) void k_dual_row_d(double *__restrict__ T, Geo 
     for (int u = 0; u < B0; u++) pq[u] = *(const d2 *)((u < npf ? D.Pbuf + (int64_t)u * g.ld : D.zrow) + jc);
     const int64_t rqv = lane < D.q ? D.rq[lane] : -1;
     const int64_t rqv1 = TWO && 64 + lane < D.q ? D.rq[64 + lane] : -1;
-    if (status != RUNNING) return;
+    // MR: every exit that computes no row sends the identity of the sum, -0
+    auto r_identity = [&]() {
+        if (MR && col) *(d2 *)(R + 2 * j2) = d2{-0.0, -0.0};
+    };
+    if (status != RUNNING) {
+        r_identity();
+        return;
+    }
     if (dp) {   // pivot t-1's objective update, as k_update applies it
         d.x = fma(cprev, pp.x, d.x);
         d.y = fma(cprev, pp.y, d.y);
@@ -105,10 +120,16 @@ __global__ __launch_bounds__(256) void k_dual_row_d(double *__restrict__ T, Geo 
             st->slot[s].status = OPTIMAL;
             st->slot[s].r = -1;
         }
+        r_identity();
         return;
     }
-    const int64_t rl = best.row - g.row0;
+    const bool own = !MR || (best.row >= g.row0 && best.row < g.row0 + g.nloc);   // uniform
+    const int64_t rl = own ? best.row - g.row0 : -1;
     if (blockIdx.x == 0 && threadIdx.x == 0) st->slot[s].r = best.row;
+    if (!own) {                              // another rank's row: its owner sends it
+        r_identity();
+        return;
+    }
     // ---- round 2: row r as stored and its pending multipliers; the chain as
     // in k_prep_d (restart at the last pending pivot on this row, every lane)
     d2 t = col ? *(const d2 *)(T + rl * g.ld + 2 * j2) : d2{0.0, 0.0};
@@ -162,6 +183,27 @@ __global__ __launch_bounds__(256) void k_dual_row_d(double *__restrict__ T, Geo 
     Cand cb{0.0, 0.0, 0, -1};
     if (col) {
         *(d2 *)(R + 2 * j2) = t;
+        ratio_cand(cb, t.x, d.x, 2 * j2, g);
+        ratio_cand(cb, t.y, d.y, 2 * j2 + 1, g);
+    }
+    if (MR) return;                          // the partials follow the exchange of R (k_dual_ratio)
+    cb = block_reduce_cand(cb);
+    if (threadIdx.x == 0) cp[blockIdx.x] = cb;
+}
+
+// MR: the ratio-test partials over the exchanged row R and the objective row
+// (row_d has applied the owed update), exactly row_d's single-rank tail.
+__global__ __launch_bounds__(256) void k_dual_ratio(const double *__restrict__ T, Geo g, const DevState *st, int s,
+                                                    const double *__restrict__ R, Cand *__restrict__ cp) {
+    constexpr int NT = 256;
+    const int64_t j2 = (int64_t)blockIdx.x * NT + threadIdx.x;
+    const bool col = j2 < (g.ncols + 1) / 2;
+    if (st->slot[s].status != RUNNING || st->slot[s].r < 0) return;   // col_d stops too
+    const int64_t rR = g.nloc + g.nobj - 1;
+    Cand cb{0.0, 0.0, 0, -1};
+    if (col) {
+        const d2 d = *(const d2 *)(T + rR * g.ld + 2 * j2);
+        const d2 t = *(const d2 *)(R + 2 * j2);
         ratio_cand(cb, t.x, d.x, 2 * j2, g);
         ratio_cand(cb, t.y, d.y, 2 * j2 + 1, g);
     }
@@ -239,7 +281,7 @@ __global__ __launch_bounds__(256) void k_dual_col_d(const double *__restrict__ T
         return;
     }
     const int64_t k = pb.key;
-    const int64_t rl = r - g.row0;
+    const int64_t rl = (r >= g.row0 && r < g.row0 + g.nloc) ? r - g.row0 : -1;   // -1: another rank's row
     const double piv = R[k];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->slot[s].k = k;
@@ -319,27 +361,55 @@ __global__ __launch_bounds__(256) void k_dual_col_d(const double *__restrict__ T
 
 static int dual_pf(int q) { return q < 16 ? 16 : q < 32 ? 32 : q < 48 ? 48 : q < 64 ? 64 : 128; }
 
-int launch_dual_pivot_d(const Launch &L, const Geo &g, DevState *st, int s, Cand *rc, int nrc, Cand *cp, int npp,
-                        double *R, const double *Pprev, const double *Cprev, double *Cs, const Defer &D,
-                        bool row_only) {
-    if (g.nobj != 1 || npp != pivot_d_blocks(g, 0, 256) || nrc != pivot_d_blocks(g, 1, 256)) return -1;
+int launch_dual_row_d(const Launch &L, const Geo &g, DevState *st, int s, const Cand *rc, int nrc, Cand *cp,
+                      double *R, const double *Pprev, const double *Cprev, const Defer &D, bool mr) {
+    if (g.nobj != 1) return -1;
+    const int npp = pivot_d_blocks(g, 0, 256);
     hipStream_t stream = (hipStream_t)L.stream;
-#define LPG_DD(PF)                                                                                                  \
-    do {                                                                                                            \
-        hipLaunchKernelGGL((k_dual_row_d<PF>), dim3(npp), dim3(256), 0, stream, g.T, g, st, s, rc, nrc, Pprev, Cprev, \
-                           R, cp, D);                                                                               \
-        if (!row_only)                                                                                              \
-            hipLaunchKernelGGL((k_dual_col_d<PF>), dim3(npp + nrc), dim3(256), 0, stream, g.T, g, st, s, s ^ 1, cp,  \
-                               npp, R, Cs, rc, npp, D);                                                             \
+#define LPG_DR(PF)                                                                                                   \
+    do {                                                                                                             \
+        if (mr)                                                                                                      \
+            hipLaunchKernelGGL((k_dual_row_d<PF, true>), dim3(npp), dim3(256), 0, stream, g.T, g, st, s, rc, nrc,    \
+                               Pprev, Cprev, R, cp, D);                                                              \
+        else                                                                                                         \
+            hipLaunchKernelGGL((k_dual_row_d<PF, false>), dim3(npp), dim3(256), 0, stream, g.T, g, st, s, rc, nrc,   \
+                               Pprev, Cprev, R, cp, D);                                                              \
     } while (0)
     switch (dual_pf(D.q)) {
-        case 16: LPG_DD(16); break;
-        case 32: LPG_DD(32); break;
-        case 48: LPG_DD(48); break;
-        case 64: LPG_DD(64); break;
-        default: LPG_DD(128); break;
+        case 16: LPG_DR(16); break;
+        case 32: LPG_DR(32); break;
+        case 48: LPG_DR(48); break;
+        case 64: LPG_DR(64); break;
+        default: LPG_DR(128); break;
     }
-#undef LPG_DD
+#undef LPG_DR
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_dual_ratio(const Launch &L, const Geo &g, const DevState *st, int s, const double *R, Cand *cp) {
+    hipLaunchKernelGGL(k_dual_ratio, dim3(pivot_d_blocks(g, 0, 256)), dim3(256), 0, (hipStream_t)L.stream, g.T, g, st,
+                       s, R, cp);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// nrc_out row blocks (>= the rows + objective rows of this rank; the same on
+// every rank of a partition, whose candidates are allgathered)
+int launch_dual_col_d(const Launch &L, const Geo &g, DevState *st, int s, const Cand *cp, const double *R, double *Cs,
+                      Cand *rc, int nrc_out, const Defer &D) {
+    const int npp = pivot_d_blocks(g, 0, 256);
+    if (g.nobj != 1 || nrc_out < pivot_d_blocks(g, 1, 256)) return -1;
+    hipStream_t stream = (hipStream_t)L.stream;
+#define LPG_DC(PF)                                                                                                   \
+    hipLaunchKernelGGL((k_dual_col_d<PF>), dim3(npp + nrc_out), dim3(256), 0, stream, g.T, g, st, s, s ^ 1, cp, npp, \
+                       R, Cs, rc, npp, D)
+    switch (dual_pf(D.q)) {
+        case 16: LPG_DC(16); break;
+        case 32: LPG_DC(32); break;
+        case 48: LPG_DC(48); break;
+        case 64: LPG_DC(64); break;
+        default: LPG_DC(128); break;
+    }
+#undef LPG_DC
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -227,15 +227,19 @@ int launch_update(const Launch &L, const Geo &g, DevState *st, int s, const doub
                   int64_t *basis, int64_t *logk, int64_t *logr, int variant, int skip);
 
 int launch_dual_rows(const Launch &L, const Geo &g, Cand *part, int nsel);
-// The dual simplex on the deferred tableau (lpg_dual.hip): k_dual_row_d over
-// npp = pivot_d_blocks(g, 0, 256) column blocks, then k_dual_col_d over npp +
-// nrc (= pivot_d_blocks(g, 1, 256)) blocks. rc: row candidates (in / out), cp:
-// ratio-test partials, R: the current pivot row, Pprev / Cprev: the previous
-// pivot's P and column (its objective update), Cs: this pivot's column.
-// row_only: k_dual_row_d alone (the owed objective update and the final peek).
-int launch_dual_pivot_d(const Launch &L, const Geo &g, DevState *st, int s, Cand *rc, int nrc, Cand *cp, int npp,
-                        double *R, const double *Pprev, const double *Cprev, double *Cs, const Defer &D,
-                        bool row_only);
+// The dual on the deferred tableau (lpg_dual.hip), one pivot = row_d, then
+// (row partition) the host's sum of R over the ranks and ratio, then col_d.
+// rc: row candidates in (nrc: every rank's after an allgather) / out
+// (nrc_out >= this rank's rows + objective rows, 256 per block), cp: the
+// ratio-test partials (one per column block), R: the current pivot row,
+// Pprev / Cprev: the previous pivot's P and column (its objective update),
+// Cs: this pivot's column. mr: row partition (R from the owner, -0 elsewhere;
+// the partials left to launch_dual_ratio).
+int launch_dual_row_d(const Launch &L, const Geo &g, DevState *st, int s, const Cand *rc, int nrc, Cand *cp,
+                      double *R, const double *Pprev, const double *Cprev, const Defer &D, bool mr);
+int launch_dual_ratio(const Launch &L, const Geo &g, const DevState *st, int s, const double *R, Cand *cp);
+int launch_dual_col_d(const Launch &L, const Geo &g, DevState *st, int s, const Cand *cp, const double *R, double *Cs,
+                      Cand *rc, int nrc_out, const Defer &D);
 int launch_dual_pivot(const Launch &L, const Geo &g, DevState *st, int s, Cand *part, int nsel, PricePart *pp,
                       int *pc, int npp, int skip, double *P, double *Cs, bool price_only = false);
 

@@ -143,3 +143,38 @@ def test_cli_dual_lp_model(tmp_path):
     g.write_text("OF {\n\tmax:z=x1\n}\nST {\n\tx1<=3;\n\tx1>=0\n}\n")
     p, lines = _cli(["--lp", str(g), "--dual"])
     assert p.returncode != 0 and "dual feasible" in json.loads(lines[-1])["error"]
+
+
+@needs_cli
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,gpus,extra", [
+    (400, 300, 2, ["--dual"]),                                   # the deferred dual over the row partition
+    (700, 500, 3, ["--dual", "--exchange", "host"]),
+    (257, 300, 2, ["--kind", "artificial"]),                      # config 5's family, two-phase
+    (640, 512, 3, ["--kind", "artificial", "--rule", "bland"]),
+])
+def test_gpus_dual_and_two_phase_equal_one_rank_and_the_oracle(m, n, gpus, extra):
+    """--dual and --kind artificial (two-phase) from plain C, one rank and
+    --gpus P (round 3: both methods run on a row partition): the same status,
+    pivot count, objective and pivot-log hash, and the oracle's."""
+    seed = 20220518
+    p1, l1 = _cli(["--synthetic", str(m), str(n)] + extra)
+    assert p1.returncode == 0, p1.stderr
+    one = json.loads(l1[-1])
+    pp, lp = _cli(["--synthetic", str(m), str(n), "--gpus", str(gpus)] + extra)
+    assert pp.returncode == 0, pp.stderr
+    assert len(lp) == 1, lp
+    dist = json.loads(lp[0])
+    method = "dual" if "--dual" in extra else "two-phase"
+    assert one["method"] == dist["method"] == method and dist["gpus"] == gpus
+    assert dist["status"] == one["status"] and dist["pivots"] == one["pivots"]
+    assert dist["objective"] == one["objective"] and dist["log_fnv"] == one["log_fnv"]
+    o = Oracle(m, n + m + 1)
+    if method == "dual":
+        o.generate(n, seed, 3)
+        res = o.solve_dual(1 << 40)
+    else:
+        o.generate(n, seed, 2)
+        res = o.solve_two_phase(1 + n + (m + 1) // 2, None, 1 << 40, 1 if "bland" in extra else 0)
+    assert res.pivots == one["pivots"] and res.objective == one["objective"]
+    assert _fnv(*o.get_log()) == one["log_fnv"]

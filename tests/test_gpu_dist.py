@@ -21,7 +21,8 @@ import threading
 import numpy as np
 import pytest
 
-from oracle.lpo import GEN_ARTIFICIAL, Oracle
+from oracle.lpo import GEN_ARTIFICIAL, GEN_DUAL, Oracle
+from util import degenerate_two_phase_lp
 
 pytestmark = pytest.mark.gpu
 
@@ -134,7 +135,8 @@ def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule, defer, monk
     assert np.array_equal(np.vstack([p["rows"] for p in parts]), T[:m])
 
 
-def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule=0, defer=None, mr=None, big_m=False):
+def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule=0, defer=None, mr=None, big_m=False,
+                 two_phase=False, dual=False):
     if defer is not None:
         os.environ["LPG_DEFER"] = defer
     if mr is not None:                            # 0: the two-kernel pair instead of k_pivot_block's multi-rank form
@@ -165,6 +167,17 @@ def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule
     if big_m:                                     # two objective rows (M part, real part)
         e.generate(n, seed, lpg.GEN_ARTIFICIAL)
         res = e.solve_big_m(1 + n + (m + 1) // 2, None, 5000, rule)
+    elif dual:                                    # the deferred dual over the row partition
+        e.generate(n, seed, lpg.GEN_DUAL)
+        res = e.solve_dual(5000)
+    elif two_phase == "degenerate":               # an artificial left basic at zero: the forced drive-out
+        T, basis, art_first = degenerate_two_phase_lp(m, n, seed)
+        e.load_rows(0, T)
+        e.set_basis(basis)
+        res = e.solve_two_phase(art_first, None, 5000, rule)
+    elif two_phase:
+        e.generate(n, seed, lpg.GEN_ARTIFICIAL)
+        res = e.solve_two_phase(1 + n + (m + 1) // 2, None, 5000, rule)
     else:
         e.generate(n, seed, kind)
         res = e.solve(5000, rule)
@@ -176,20 +189,35 @@ def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule
     dist.destroy_process_group()
 
 
-def _processes(world, m, n, seed, push, kind=0, rule=0, defer=None, mr=None, big_m=False):
+def _processes(world, m, n, seed, push, kind=0, rule=0, defer=None, mr=None, big_m=False, two_phase=False, dual=False):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_gloo_worker, args=(world, port, m, n, seed, d, push, kind, rule, defer, mr, big_m), nprocs=world,
-                 join=True)
+        mp.spawn(_gloo_worker, args=(world, port, m, n, seed, d, push, kind, rule, defer, mr, big_m, two_phase, dual),
+                 nprocs=world, join=True)
         parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     if big_m:
         o = Oracle(m, n + m + 1, nobj=2)
         o.generate(n, seed, GEN_ARTIFICIAL)
         ores = o.solve_big_m(1 + n + (m + 1) // 2, None, 5000, rule)
+    elif dual:
+        o = Oracle(m, n + m + 1)
+        o.generate(n, seed, GEN_DUAL)
+        ores = o.solve_dual(5000)
+        assert ores.status == 1 and ores.pivots > 0
+    elif two_phase == "degenerate":
+        T0, basis, art_first = degenerate_two_phase_lp(m, n, seed)
+        o = Oracle(m, n + m + 1)
+        o.load_tableau(T0, basis)
+        ores = o.solve_two_phase(art_first, None, 5000, rule)
+        assert ores.status == 1                   # OPTIMAL (after the drive-out)
+    elif two_phase:
+        o = Oracle(m, n + m + 1)
+        o.generate(n, seed, GEN_ARTIFICIAL)
+        ores = o.solve_two_phase(1 + n + (m + 1) // 2, None, 5000, rule)
     else:
         o = Oracle(m, n + m + 1)
         o.generate(n, seed, kind)
@@ -216,6 +244,30 @@ def test_processes_big_m_bitwise(lpg, world, m, n, rule, push, mr):
     NOBJ = 2 form) and with the pair -- bitwise the oracle."""
     parts = _processes(world, m, n, 9, push=push, rule=rule, mr=mr, big_m=True)
     assert all((p["wg"] > 0) == (push and mr is None) for p in parts)
+
+
+@pytest.mark.parametrize("push,mr", [(False, None), (True, None), (True, "0")])
+@pytest.mark.parametrize("world,m,n,rule,seed,lp", [(2, 257, 300, 0, 9, "gen"), (3, 640, 512, 1, 9, "gen"),
+                                                    (2, 64, 80, 0, 1, "degenerate"), (3, 257, 300, 0, 2, "degenerate"),
+                                                    (2, 300, 200, 1, 3, "degenerate")])
+def test_processes_two_phase_bitwise(lpg, world, m, n, rule, seed, lp, push, mr):
+    """Two-phase over 2-3 processes (round 3; single rank before): phase I on
+    the artificial objective, the |b| test summed over ranks in global row
+    order, forced pivots driving basic artificials out (each row's owner finds
+    the column), phase II -- status, pivot count, log, basis, every row and the
+    objective row bitwise the oracle's."""
+    _processes(world, m, n, seed, push=push, rule=rule, mr=mr, two_phase=lp)
+
+
+@pytest.mark.parametrize("world,m,n,seed,defer", [(2, 100, 150, 3, None), (3, 400, 300, 3, None), (2, 257, 200, 5, "5"),
+                                                  (3, 700, 500, 7, "32"), (2, 1000, 800, 3, "128")])
+def test_processes_dual_bitwise(lpg, world, m, n, seed, defer):
+    """The deferred dual simplex over 2-3 processes (round 3; single rank
+    before): row candidates allgathered, the leaving row summed from its owner
+    (-0 elsewhere), the ratio test on every rank over the replicated row, each
+    rank's rows through its own chain and block pass -- status, pivot count,
+    log, basis, every row and the objective row bitwise the oracle's."""
+    _processes(world, m, n, seed, push=False, defer=defer, dual=True)
 
 
 @pytest.mark.parametrize("mr", [None, "0"])

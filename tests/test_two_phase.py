@@ -13,7 +13,7 @@ import pytest
 
 from oracle.lpo import GEN_ARTIFICIAL, RULE_BLAND, RULE_DANTZIG, Oracle
 from tests.golden.make_golden import synthetic
-from util import STATUS
+from util import STATUS, degenerate_two_phase_lp
 
 # A5 of SURVEY.md Appendix A (lack row 0): max x1 + 2 x2; x1 + x2 = 3; x1 - x2 <= 1.
 # Columns [b | x1 x2 x3(slack) | a1(artificial for row 0)]
@@ -60,6 +60,35 @@ def test_config5_family_matches_highs(m, n, rule):
         assert abs(r.objective - (-hs.fun)) <= 1e-9 * abs(hs.fun)
         assert all(b < art_first for b in o.get_basis())
 
+
+
+@pytest.mark.parametrize("m,n,seed,rule", [(64, 80, 1, RULE_DANTZIG), (257, 300, 2, RULE_DANTZIG), (300, 200, 3, RULE_BLAND)])
+def test_degenerate_lp_needs_the_drive_out(m, n, seed, rule):
+    """The fixture of the multi-rank drive-out tests does what it says: phase I
+    stops OPTIMAL with E2's artificial basic at zero and a usable (negative)
+    original entry in its row; the two-phase solve then ends OPTIMAL with no
+    artificial basic, and its optimum equals HiGHS on the same LP."""
+    T, basis, art = degenerate_two_phase_lp(m, n, seed)
+    N = n + m
+    o = _oracle(T, basis)
+    c1 = np.zeros(N)
+    c1[art - 1:] = -1.0
+    o.set_active_columns(N)
+    o.set_objective(c1)
+    r1 = o.solve(5000, rule)
+    b = o.get_basis()
+    assert r1.status == STATUS["OPTIMAL"] and r1.objective == 0.0
+    assert [i for i in range(m) if b[i] >= art] == [m - 1]
+    assert o.get_rows(m - 1, 1)[0, 3] == -1.0
+    o = _oracle(T, basis)
+    r = o.solve_two_phase(art, None, 5000, rule)
+    assert r.status == STATUS["OPTIMAL"] and all(x < art for x in o.get_basis())
+    from scipy.optimize import linprog
+    A, bb = T[:m, 1:art], T[:m, 0]
+    eq = np.zeros(m, dtype=bool)
+    eq[[1, m - 1]] = True
+    hs = linprog(-(-T[m, 1:art]), A_ub=A[~eq], b_ub=bb[~eq], A_eq=A[eq], b_eq=bb[eq], bounds=(0, None), method="highs")
+    assert hs.status == 0 and abs(r.objective - (-hs.fun)) <= 1e-9 * abs(hs.fun)
 
 # ---------------------------------------------------------------- GPU ----
 
@@ -122,4 +151,19 @@ def test_gpu_forced_pivot_matches_oracle(lpg):
     _same(e, o, m)
     with pytest.raises(lpg.LPGError):
         e.pivot(1 + n + 30, 2)            # slack of row 30: zero in row 2 -> refused, nothing applied
+    _same(e, o, m)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,seed,rule", [(64, 80, 1, RULE_DANTZIG), (300, 200, 3, RULE_BLAND)])
+def test_gpu_two_phase_drive_out_bitwise(lpg, m, n, seed, rule):
+    """An artificial left basic at zero after phase I, driven out by a forced
+    (negative) pivot, on one rank: bitwise the oracle."""
+    T, basis, art = degenerate_two_phase_lp(m, n, seed)
+    e = lpg.Engine(m, n + m + 1)
+    e.load_tableau(T, basis)
+    r = e.solve_two_phase(art, None, 5000, rule)
+    o = _oracle(T, basis)
+    ro = o.solve_two_phase(art, None, 5000, rule)
+    assert r.status == ro.status == STATUS["OPTIMAL"] and r.pivots == ro.pivots and r.objective == ro.objective
     _same(e, o, m)

@@ -44,3 +44,33 @@ def transcripts():
 
 def pivots_of(case_rule):
     return [tuple(p) for p in case_rule["pivots"]]
+
+
+def degenerate_two_phase_lp(m, n, seed):
+    """A two-phase LP whose phase I ends with an artificial basic at zero that
+    a forced pivot must drive out: <= rows with slack units, plus two equality
+    rows with artificial units (the last two columns), E1 (row 1): x1 = 1 and
+    E2 (row m-1): x1 - x3 = 1. Phase I enters x1 on E1 (the ratio tie goes to
+    the smaller row), leaving E2's artificial basic at zero with T[E2][x3] = -1
+    and d_x3 = +1, so phase I stops OPTIMAL and the drive-out pivots x3 into E2
+    (a negative pivot). Returns (T with the objective row [0 | -c | 0], basis,
+    art_first)."""
+    rng = np.random.default_rng(seed)
+    N = n + m
+    T = np.zeros((m + 1, N + 1))
+    eq = (1, m - 1)
+    le = [i for i in range(m) if i not in eq]
+    basis = np.zeros(m, dtype=np.int64)
+    for s, i in enumerate(le):
+        T[i, 0] = n / 8 * (1 + rng.random())
+        T[i, 1:n + 1] = rng.random(n)
+        T[i, n + 1 + s] = 1.0
+        basis[i] = n + 1 + s
+    art_first = n + 1 + len(le)
+    T[1, [0, 1, art_first]] = 1.0
+    basis[1] = art_first
+    T[m - 1, [0, 1, art_first + 1]] = 1.0
+    T[m - 1, 3] = -1.0
+    basis[m - 1] = art_first + 1
+    T[m, 1:n + 1] = -(1 + rng.random(n))
+    return T, basis, art_first
