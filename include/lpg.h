@@ -265,7 +265,10 @@ int  lpg_solve_big_m(lpg_ctx *ctx, int64_t art_first, const double *cost, int64_
  * Leaving row: most negative b_i < -eps_opt (ties: smallest row); entering
  * column: min d_j / (-a_rj) over a_rj < -eps_piv (ties: smallest j); none ->
  * LPG_INFEASIBLE; no negative b -> LPG_OPTIMAL. Same update kernel and
- * arithmetic as the primal loop. Single rank. */
+ * arithmetic as the primal loop. On a row partition (round 3) every rank
+ * calls it (collective) and the deferred form runs: the row candidates are
+ * allgathered and the leaving row is summed from its owner; LPG_FLAG_EAGER
+ * is single rank. */
 int  lpg_solve_dual(lpg_ctx *ctx, int64_t max_pivots, lpg_result *out);
 
 /* ---- readout ---- */
