@@ -267,7 +267,7 @@ def test_processes_dual_bitwise(lpg, world, m, n, seed, defer):
     (-0 elsewhere), the ratio test on every rank over the replicated row, each
     rank's rows through its own chain and block pass -- status, pivot count,
     log, basis, every row and the objective row bitwise the oracle's."""
-    _processes(world, m, n, seed, push=False, defer=defer, dual=True)
+    _processes(world, m, n, seed, push=world == 2, defer=defer, dual=True)   # the push attached: unused, harmless
 
 
 @pytest.mark.parametrize("mr", [None, "0"])
@@ -312,6 +312,37 @@ def test_rccl_single_rank_communicator(lpg, m, n, defer, graphs, monkeypatch):
     assert res.status == ores.status == 1 and res.pivots == ores.pivots and res.objective == ores.objective
     assert np.array_equal(e.get_log()[0], o.get_log()[0]) and np.array_equal(e.get_log()[1], o.get_log()[1])
     assert np.array_equal(e.get_rows(0, m + 1), o.get_rows())
+
+
+@pytest.mark.parametrize("method", ["dual", "two_phase", "two_phase_degenerate"])
+def test_rccl_single_rank_dual_and_two_phase(lpg, method):
+    """The dual and two-phase on a 1-rank RCCL communicator: the partition
+    code path (row candidates through ncclAllGather, the leaving row and the
+    |b| running sum through ncclAllReduce, the drive-out column shared) runs
+    for real and equals the oracle bit for bit."""
+    m, n = 400, 300
+    e = lpg.Engine(m, n + m + 1)
+    e.comm_init_rccl(lpg.Engine.rccl_unique_id())
+    o = Oracle(m, n + m + 1)
+    if method == "dual":
+        e.generate(n, 3, lpg.GEN_DUAL)
+        o.generate(n, 3, GEN_DUAL)
+        res, ores = e.solve_dual(100_000), o.solve_dual(100_000)
+    elif method == "two_phase":
+        e.generate(n, 9, lpg.GEN_ARTIFICIAL)
+        o.generate(n, 9, GEN_ARTIFICIAL)
+        art = 1 + n + (m + 1) // 2
+        res, ores = e.solve_two_phase(art, None, 100_000, 1), o.solve_two_phase(art, None, 100_000, 1)
+    else:
+        T, basis, art = degenerate_two_phase_lp(m, n, 2)
+        e.load_rows(0, T)
+        e.set_basis(basis)
+        o.load_tableau(T, basis)
+        res, ores = e.solve_two_phase(art, None, 100_000, 0), o.solve_two_phase(art, None, 100_000, 0)
+    assert res.status == ores.status and res.pivots == ores.pivots and res.objective == ores.objective
+    assert np.array_equal(e.get_log()[0], o.get_log()[0]) and np.array_equal(e.get_log()[1], o.get_log()[1])
+    assert np.array_equal(e.get_rows(0, m + 1), o.get_rows())
+    assert np.array_equal(e.get_basis(), o.get_basis())
 
 
 def test_host_comm_single_rank(lpg):
