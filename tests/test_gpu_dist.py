@@ -293,6 +293,19 @@ def test_processes_owner_push_bitwise(lpg, world, m, n, kind, rule, defer, mr):
     assert len({p["wg"] for p in parts}) == 1          # the same slices on every rank
 
 
+@pytest.mark.parametrize("world,m,n,kind,rule,defer,mr", [(4, 1024, 2048, 0, 0, None, None), (8, 1024, 2048, 0, 0, None, None),
+                                                          (8, 203, 301, 0, 0, "32", "0"), (4, 700, 900, 1, 1, "64", None)])
+def test_processes_owner_push_4_and_8_ranks(lpg, world, m, n, kind, rule, defer, mr):
+    """The driver's N = 4 and N = 8 layouts rehearsed on one GPU: 4 and 8
+    processes (config 2's shape: 8 x 13 persistent workgroups are resident
+    together), the owner push with the multi-rank pivot launch or the pair,
+    the candidate words of every rank (6 lanes per rank in xpoll_best, rows
+    of 128-256 per rank) -- bitwise the oracle."""
+    parts = _processes(world, m, n, 778, push=True, kind=kind, rule=rule, defer=defer, mr=mr)
+    assert all((p["wg"] > 0) == (mr is None) for p in parts)
+    assert len({p["wg"] for p in parts}) == 1
+
+
 @pytest.mark.parametrize("m,n,defer,graphs", [(300, 500, None, "0"), (1024, 2048, None, "0"), (1024, 2048, "64", "0"),
                                               (1024, 2048, "128", "0"), (1024, 2048, None, "1")])
 def test_rccl_single_rank_communicator(lpg, m, n, defer, graphs, monkeypatch):
@@ -380,3 +393,35 @@ def test_owner_push_single_rank(lpg, m, n, mr, monkeypatch):
     assert res.status == ores.status == 1 and res.pivots == ores.pivots and res.objective == ores.objective
     assert np.array_equal(e.get_log()[0], o.get_log()[0]) and np.array_equal(e.get_log()[1], o.get_log()[1])
     assert np.array_equal(e.get_rows(0, m + 1), o.get_rows())
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_bench_torchrun_4_and_8_ranks(world):
+    """bench.py as the driver launches it for N > 1 (torch.distributed.run,
+    one process per rank, 127.0.0.1 rendezvous), rehearsed on one GPU at
+    config 2 (host collectives for setup: RCCL refuses ranks sharing a GPU):
+    exactly one JSON line on stdout, the owner push attached and the
+    persistent multi-rank launch on every rank (no fallback to the
+    collectives), the ranks' replicated logs agreeing after the warm-up."""
+    import json
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(world),
+           "--config", "2", "--host-comm", "--steps", "4", "--warmup", "1", "--no-cpu"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["value"] > 0 and d["status"] == "ITER_LIMIT"
+    assert "owner push" in d["config"]["parallelism"], d["config"]
+    assert d["config"]["pivot_loop"].startswith("k_pivot_block"), d["config"]
+    assert d["config"]["pivots_timed"] > 0 and d["config"]["pivots_timed"] % 4 == 0
+    assert "using the collectives" not in p.stderr
