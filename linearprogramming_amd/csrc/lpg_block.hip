@@ -108,11 +108,12 @@ __device__ __forceinline__ u4 pack(uint64_t a, uint32_t b, uint32_t tag) {
 __device__ __forceinline__ uint64_t lo64(const u4 &v) { return ((uint64_t)v.y << 32) | v.x; }
 
 // One wave sweeps the NG-granule records of nwg workgroups until every tag
-// equals `tag`; lane l holds records l, l + 64, l + 128, l + 192. False on
-// timeout (the caller stops the launch).
-template <int NG>
+// equals `tag`; lane l holds records l, l + 64, l + 128, l + 192. XG: lane 0
+// also holds the one extra granule nwg * NG (workgroup 0's P_q[0]) in xg.
+// False on timeout (the caller stops the launch).
+template <int NG, bool XG = false>
 __device__ bool sweep(__amdgpu_buffer_rsrc_t r, int nwg, uint32_t tag, u4 (&rec)[kPer][NG], int phase,
-                      DevState *st) {
+                      DevState *st, u4 *xg = nullptr) {
     const int lane = threadIdx.x & 63;
     const long long t0 = (long long)wall_clock64();
     for (;;) {
@@ -125,6 +126,14 @@ __device__ bool sweep(__amdgpu_buffer_rsrc_t r, int nwg, uint32_t tag, u4 (&rec)
             if (w < nwg) {
 #pragma unroll
                 for (int k = 0; k < NG; k++) rec[p][k] = rec_load(r, (w * NG + k) * 16);
+            }
+        }
+        if (XG && lane == 0) {
+            *xg = rec_load(r, nwg * NG * 16);
+            if (xg->w != tag) {
+                ok = false;
+                bad = nwg * NG;
+                seen = xg->w;
             }
         }
 #pragma unroll
@@ -438,8 +447,14 @@ struct BlockArgs {
 // rank's), the replicated basis / lv are kept by workgroup 0 of every rank.
 template <int RULE, int NOBJ, bool MR>
 __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
-    // pricing record granules: {key, j} {dR, phys} {P_q[phys]} {P_q[0] (workgroup 0)} [{dM}]
-    constexpr int NGP = NOBJ == 2 ? 5 : 4;
+    // pricing record granules: {key, j} {P_q[phys], phys} [{dR}] [{dM}], and one
+    // extra granule {P_q[0]} after the nwg records (workgroup 0's). Dantzig on
+    // one objective row carries no dR: the key holds it (cls 0, ~bits(dR) in the
+    // low 63 bits), so the record a sweep reads is 32 bytes, not 64.
+    constexpr bool KDR = RULE != RULE_BLAND && NOBJ == 1;    // dR recovered from the key
+    constexpr int GDR = KDR ? 0 : 2;                         // granule of dR (0: none)
+    constexpr int NGP = 2 + (KDR ? 0 : 1) + (NOBJ == 2 ? 1 : 0);
+    static_assert(NGP < kRecPMax, "pricing records (nwg * NGP + 1 granules) exceed their reservation");
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ Bcast bc;
     __shared__ int xok;
@@ -467,7 +482,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     const int64_t i = (int64_t)wg * rw + tid;          // this thread's local constraint row
     const bool hr = tid < rw && i < g.nloc;
     const int64_t rM = g.nloc, rR = g.nloc + NOBJ - 1;
-    const __amdgpu_buffer_rsrc_t recP = rsrc(a.rec, nwg * NGP * 16);
+    const __amdgpu_buffer_rsrc_t recP = rsrc(a.rec, (nwg * NGP + 1) * 16);
     const __amdgpu_buffer_rsrc_t recR = rsrc(a.rec + nwg * kRecPMax, nwg * kRecR * 16);
     DevState *st = a.st;
 
@@ -792,38 +807,39 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             }
             rec_store(recP, (wg * NGP + 0) * 16, pack(h, l, tag));
             // P_q[0] for every slice's column 0 (workgroup 0 holds column 0 in thread 0)
-            rec_store(recP, (wg * NGP + 3) * 16, pack((uint64_t)__double_as_longlong(wg == 0 ? pq : 0.0), 0u, tag));
+            if (wg == 0) rec_store(recP, (nwg * NGP) * 16, pack((uint64_t)__double_as_longlong(pq), 0u, tag));
         }
         // the slice winner's objective entries and P_q entry ride along (C_{t+1}[obj]
         // and P_q[k] if it wins the grid); the thread of that column holds them
         if (pb.j >= 0 && hc && (int64_t)lj == pb.j) {
-            rec_store(recP, (wg * NGP + 1) * 16, pack((uint64_t)__double_as_longlong(dR), (uint32_t)c, tag));
-            rec_store(recP, (wg * NGP + 2) * 16, pack((uint64_t)__double_as_longlong(pq), 0u, tag));
-            if (NOBJ == 2) rec_store(recP, (wg * NGP + 4) * 16, pack((uint64_t)__double_as_longlong(dM), 0u, tag));
+            rec_store(recP, (wg * NGP + 1) * 16, pack((uint64_t)__double_as_longlong(pq), (uint32_t)c, tag));
+            if (!KDR) rec_store(recP, (wg * NGP + GDR) * 16, pack((uint64_t)__double_as_longlong(dR), 0u, tag));
+            if (NOBJ == 2) rec_store(recP, (wg * NGP + NGP - 1) * 16, pack((uint64_t)__double_as_longlong(dM), 0u, tag));
         }
         if (pb.j < 0 && tid == 0) {
-            rec_store(recP, (wg * NGP + 1) * 16, pack(0ull, 0u, tag));
-            rec_store(recP, (wg * NGP + 2) * 16, pack(0ull, 0u, tag));
-            if (NOBJ == 2) rec_store(recP, (wg * NGP + 4) * 16, pack(0ull, 0u, tag));
+#pragma unroll
+            for (int k = 1; k < NGP; k++) rec_store(recP, (wg * NGP + k) * 16, pack(0ull, 0u, tag));
         }
         LPG_BPUB(0, t);
         LPG_BPH(t, 3);
 
         // ================= phase S: the entering column and the ratio test
         if (wave == 0) {
-            u4 rec[kPer][NGP], pay[NGP - 1];
-            const bool ok = sweep<NGP>(recP, nwg, tag, rec, 2, st);
+            u4 rec[kPer][NGP], pay[NGP - 1], xg{0u, 0u, 0u, 0u};
+            const bool ok = sweep<NGP, true>(recP, nwg, tag, rec, 2, st, &xg);
             uint64_t h = ~0ull, p0 = 0, p1 = 0, p2 = 0, p3 = 0;
             uint32_t l = ~0u;
             int src = -1;
             if (ok) {
                 rec_min<NGP>(rec, nwg, h, l, src, pay);
-                p0 = lo64(pay[0]);              // dR at the entering column
+                // dR at the entering column: from the key (v < 0: sign bit set,
+                // ~bits(v) in the low 63 bits) or its own granule
+                p0 = KDR ? ((1ull << 63) | (~h & 0x7fffffffffffffffull)) : lo64(pay[GDR - 1]);
                 p1 = pay[0].z;                  // its physical column
-                p2 = lo64(pay[1]);              // P_q at the entering column
+                p2 = lo64(pay[0]);              // P_q at the entering column
                 if (NOBJ == 2) p3 = lo64(pay[NGP - 2]);   // dM
-                // P_q[0]: workgroup 0's record, held by lane 0
-                if (lane == 0) bc.z = lo64(rec[0][3]);
+                // P_q[0]: workgroup 0's extra granule, held by lane 0
+                if (lane == 0) bc.z = lo64(xg);
             }
             if (lane == 0) {
                 bc.h = h;
