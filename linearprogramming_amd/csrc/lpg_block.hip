@@ -213,6 +213,8 @@ struct Bcast {            // one phase's decision, from wave 0 to the workgroup
     int32_t ok;           // 1: decided, 0: none (OPTIMAL / UNBOUNDED), -1: timeout, -2: exchange timeout
     uint64_t p0, p1, p2, p3;   // winner payload
     uint64_t z;           // P_q[0]
+    uint64_t pv;          // phase P, RPIV: the pivot element, fetched after the sweep
+    int32_t okv;          //   1: fetched, -1: timeout
 };
 
 // Multi-rank (owner-push exchange, Xch, lpg_internal.h). Workgroup 0 of every
@@ -454,6 +456,12 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     constexpr bool KDR = RULE != RULE_BLAND && NOBJ == 1;    // dR recovered from the key
     constexpr int GDR = KDR ? 0 : 2;                         // granule of dR (0: none)
     constexpr int NGP = 2 + (KDR ? 0 : 1) + (NOBJ == 2 ? 1 : 0);
+    // ratio records: {theta, key} {piv, row}; one rank under Dantzig (key ==
+    // row) sweeps only {theta, row} and fetches the winner's {piv, row} granule
+    // (granule nwg + w) while the pivot row's base entries load -- the pivot
+    // element is first needed after the chain
+    constexpr bool RPIV = !MR && RULE != RULE_BLAND;
+    constexpr int NGR = RPIV ? 1 : kRecR;
     static_assert(NGP < kRecPMax, "pricing records (nwg * NGP + 1 granules) exceed their reservation");
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ Bcast bc;
@@ -559,6 +567,9 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         // the grid's best is awaited every workgroup computes the pivot row
         // of this rank's best row -- which is the grid's whenever this rank
         // holds the grid's (the global minimum is one of the ranks' minima)
+        u4 pvg{0u, 0u, 0u, 0u};                         // RPIV, wave 0 lane 0: the winner's {piv, row} granule
+        bool pvneed = false;                            // RPIV, wave 0: it is still to be checked
+        int psrc = -1;
         if (wave == 0) {
             uint64_t h = ~0ull, p0 = 0, p1 = 0;
             uint32_t l = ~0u;
@@ -590,30 +601,69 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                     p1 = rdl64(mp1, wl);
                 }
             } else {
-                u4 rec[kPer][kRecR], pay[kRecR - 1];
-                ok = sweep<kRecR>(recR, nwg, tag - 1, rec, 1, st);
+                u4 rec[kPer][NGR], pay[NGR > 1 ? NGR - 1 : 1];
+                ok = sweep<NGR>(recR, nwg, tag - 1, rec, 1, st);
                 if (ok) {
-                    rec_min<kRecR>(rec, nwg, h, l, src, pay);
-                    p0 = lo64(pay[0]);          // pivot element
-                    p1 = pay[0].z;              // leaving row
+                    rec_min<NGR>(rec, nwg, h, l, src, pay);
+                    if (RPIV) {
+                        p1 = l;                 // leaving row (the key)
+                        if (src >= 0 && lane == 0) pvg = rec_load(recR, (nwg + src) * 16);   // checked below
+                        pvneed = src >= 0;
+                    } else {
+                        p0 = lo64(pay[0]);      // pivot element
+                        p1 = pay[0].z;          // leaving row
+                    }
                 }
             }
             if (MR && wg == 0 && ok && lane == 0)   // this rank's best -> every rank
                 xpush_best(a.X, a.xtag0 + (uint32_t)t, src >= 0 ? h : ~0ull, src >= 0 ? l : ~0u, p0, p1);
+            psrc = src;
             if (lane == 0) {
                 bc.h = h;
                 bc.l = l;
                 bc.ok = !ok ? -1 : (src >= 0 ? 1 : 0);
                 bc.p0 = p0;
                 bc.p1 = p1;
+                bc.pv = p0;
+                bc.okv = 1;
             }
         }
         __syncthreads();
         LPG_BPH(t, 1);
         int okP = bc.ok;
-        double piv = __longlong_as_double((long long)bc.p0);
         int64_t r = (int64_t)bc.p1;                     // leaving row (MR: this rank's candidate so far)
+        const int64_t rs = r;                           // MR: the row computed ahead of the decision
+        const bool owns = okP > 0 && (!MR || (rs >= g.row0 && rs < g.row0 + g.nloc));
+        // this slice's base entries of row rs and the multipliers -C_u[rs]
+        // (lane u < q; -0 past q): in flight across the barrier below
+        const int64_t rloc = owns ? rs - g.row0 : -1;
+        const double xrow = (owns && hc) ? g.T[rloc * g.ld + c] : 0.0;
+        const double mrow = (owns && lane < q) ? -ld_wt(D.Cbuf + (int64_t)lane * D.cs + rloc) : -0.0;
+        if (RPIV && pvneed) {
+            // the winner's {piv, row} granule: stored with its {theta, row}, so
+            // normally already visible; re-polled (bounded) if not
+            const long long t0 = (long long)wall_clock64();
+            int okv = 1;
+            if (lane == 0) {
+                while (pvg.w != tag - 1 || (int64_t)pvg.z != r) {
+                    if ((long long)wall_clock64() - t0 > kSpinTicks) {
+                        okv = -1;
+                        st->stall_info[0] = 7;
+                        st->stall_info[1] = tag - 1;
+                        st->stall_info[2] = nwg + psrc;
+                        st->stall_info[3] = pvg.w;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    pvg = rec_load(recR, (nwg + psrc) * 16);
+                }
+                bc.pv = lo64(pvg);
+                bc.okv = okv;
+            }
+        }
         __syncthreads();                                // bc is rewritten below / by the next phase
+        double piv = __longlong_as_double((long long)bc.pv);
+        if (RPIV && bc.okv < 0) okP = -1;
         auto fail_p = [&](int ok) {                     // the oracle's NUMERIC rule (k_prep_d), UNBOUNDED, timeouts
             if (wg == 0 && tid == 0) {
                 const int32_t sv = ok < 0 ? NUMERIC : (ok == 0 ? UNBOUNDED : NUMERIC);
@@ -631,10 +681,10 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         // the multipliers -C_u[rr] (lane u < q; -0 past q), the restart point
         // (the last pending pivot on rr), the base entries, the pending chain
         auto pivot_row = [&](bool on, int64_t rr) -> double {
-            wm[wave][lane] = (on && lane < q) ? -ld_wt(D.Cbuf + (int64_t)lane * D.cs + rr) : -0.0;
+            wm[wave][lane] = mrow;
             const unsigned long long hit = __ballot(on && lane < q && rqv == rr);
             const int qs = hit ? 63 - __clzll((long long)hit) : -1;
-            double x = (on && hc) ? g.T[rr * g.ld + c] : 0.0;
+            double x = xrow;
             if (qs >= 0) x = sPt[qs];
             const double *wmw = &wm[wave][0];
             if (!on) {
@@ -652,9 +702,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             }
             return x;
         };
-        const int64_t rs = r;                           // MR: the row computed ahead of the decision
-        const bool owns = okP > 0 && (!MR || (rs >= g.row0 && rs < g.row0 + g.nloc));
-        double x = pivot_row(owns, owns ? rs - g.row0 : -1);
+        double x = pivot_row(owns, rloc);
         LPG_BPH(t, 2);
         const uint32_t xt = a.xtag0 + (uint32_t)t;      // MR: this pivot's exchange tag
         const int xpar = (int)(xt & 1);
@@ -931,8 +979,8 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                 h = (uint64_t)__double_as_longlong(cd.theta);
                 l = (uint32_t)cd.key;
             }
-            rec_store(recR, (wg * kRecR + 0) * 16, pack(h, l, tag));
-            rec_store(recR, (wg * kRecR + 1) * 16,
+            rec_store(recR, (wg * NGR + 0) * 16, pack(h, l, tag));
+            rec_store(recR, ((RPIV ? nwg : 0) + wg * NGR + (RPIV ? 0 : 1)) * 16,
                       pack((uint64_t)__double_as_longlong(cd.piv), (uint32_t)cd.row, tag));
             if (last) a.part[wg] = cd;
         }
