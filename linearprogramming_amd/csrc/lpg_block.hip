@@ -109,11 +109,11 @@ __device__ __forceinline__ uint64_t lo64(const u4 &v) { return ((uint64_t)v.y <<
 
 // One wave sweeps the NG-granule records of nwg workgroups until every tag
 // equals `tag`; lane l holds records l, l + 64, l + 128, l + 192. XG: lane 0
-// also holds the one extra granule nwg * NG (workgroup 0's P_q[0]) in xg.
+// also holds the one extra granule xidx (workgroup 0's P_q[0]) in xg.
 // False on timeout (the caller stops the launch).
 template <int NG, bool XG = false>
 __device__ bool sweep(__amdgpu_buffer_rsrc_t r, int nwg, uint32_t tag, u4 (&rec)[kPer][NG], int phase,
-                      DevState *st, u4 *xg = nullptr) {
+                      DevState *st, u4 *xg = nullptr, int xidx = 0) {
     const int lane = threadIdx.x & 63;
     const long long t0 = (long long)wall_clock64();
     for (;;) {
@@ -129,10 +129,10 @@ __device__ bool sweep(__amdgpu_buffer_rsrc_t r, int nwg, uint32_t tag, u4 (&rec)
             }
         }
         if (XG && lane == 0) {
-            *xg = rec_load(r, nwg * NG * 16);
+            *xg = rec_load(r, xidx * 16);
             if (xg->w != tag) {
                 ok = false;
-                bad = nwg * NG;
+                bad = xidx;
                 seen = xg->w;
             }
         }
@@ -463,6 +463,11 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     constexpr bool RPIV = !MR && RULE != RULE_BLAND;
     constexpr int NGR = RPIV ? 1 : kRecR;
     static_assert(NGP < kRecPMax, "pricing records (nwg * NGP + 1 granules) exceed their reservation");
+    // PK1 (KDR): the sweep reads one granule per workgroup, {key, physical
+    // column}; the winner's {P_q[phys], j} granule (nwg + w) is fetched after
+    // the sweep while the entering column's base entries load (j, the tie-break,
+    // is read for every record that shares the least key -- rare)
+    constexpr bool PK1 = KDR;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ Bcast bc;
     __shared__ int xok;
@@ -491,6 +496,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     const bool hr = tid < rw && i < g.nloc;
     const int64_t rM = g.nloc, rR = g.nloc + NOBJ - 1;
     const __amdgpu_buffer_rsrc_t recP = rsrc(a.rec, (nwg * NGP + 1) * 16);
+    const int xidx = PK1 ? 2 * nwg : nwg * NGP;                // workgroup 0's {P_q[0]} granule
     const __amdgpu_buffer_rsrc_t recR = rsrc(a.rec + nwg * kRecPMax, nwg * kRecR * 16);
     DevState *st = a.st;
 
@@ -853,18 +859,29 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                                           (~(uint64_t)__double_as_longlong(pb.v) & 0x7fffffffffffffffull));
                 l = (uint32_t)pb.j;
             }
-            rec_store(recP, (wg * NGP + 0) * 16, pack(h, l, tag));
+            if (!PK1) rec_store(recP, (wg * NGP + 0) * 16, pack(h, l, tag));
+            else if (pb.j < 0) {
+                rec_store(recP, wg * 16, pack(h, l, tag));
+                rec_store(recP, (nwg + wg) * 16, pack(0ull, ~0u, tag));
+            }
             // P_q[0] for every slice's column 0 (workgroup 0 holds column 0 in thread 0)
-            if (wg == 0) rec_store(recP, (nwg * NGP) * 16, pack((uint64_t)__double_as_longlong(pq), 0u, tag));
+            if (wg == 0) rec_store(recP, xidx * 16, pack((uint64_t)__double_as_longlong(pq), 0u, tag));
         }
         // the slice winner's objective entries and P_q entry ride along (C_{t+1}[obj]
         // and P_q[k] if it wins the grid); the thread of that column holds them
-        if (pb.j >= 0 && hc && (int64_t)lj == pb.j) {
+        if (PK1 && pb.j >= 0 && hc && (int64_t)lj == pb.j) {
+            // the slice winner's thread: {key, physical column} and {P_q there, j}
+            const uint64_t h = ((uint64_t)(uint32_t)pb.cls << 63) |
+                               (~(uint64_t)__double_as_longlong(pb.v) & 0x7fffffffffffffffull);
+            rec_store(recP, wg * 16, pack(h, (uint32_t)c, tag));
+            rec_store(recP, (nwg + wg) * 16, pack((uint64_t)__double_as_longlong(pq), (uint32_t)pb.j, tag));
+        }
+        if (!PK1 && pb.j >= 0 && hc && (int64_t)lj == pb.j) {
             rec_store(recP, (wg * NGP + 1) * 16, pack((uint64_t)__double_as_longlong(pq), (uint32_t)c, tag));
             if (!KDR) rec_store(recP, (wg * NGP + GDR) * 16, pack((uint64_t)__double_as_longlong(dR), 0u, tag));
             if (NOBJ == 2) rec_store(recP, (wg * NGP + NGP - 1) * 16, pack((uint64_t)__double_as_longlong(dM), 0u, tag));
         }
-        if (pb.j < 0 && tid == 0) {
+        if (!PK1 && pb.j < 0 && tid == 0) {
 #pragma unroll
             for (int k = 1; k < NGP; k++) rec_store(recP, (wg * NGP + k) * 16, pack(0ull, 0u, tag));
         }
@@ -872,9 +889,88 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         LPG_BPH(t, 3);
 
         // ================= phase S: the entering column and the ratio test
-        if (wave == 0) {
+        u4 g1{0u, 0u, 0u, 0u};                          // PK1, wave 0 lane 0: the winner's {P_q[k], j}
+        int g1src = -1;                                 // PK1, wave 0: its workgroup, -1 if fetched already / none
+        if (wave == 0 && PK1) {
+            u4 rec[kPer][1], xg{0u, 0u, 0u, 0u};
+            const bool ok = sweep<1, true>(recP, nwg, tag, rec, 2, st, &xg, xidx);
+            uint64_t hmin = ~0ull, p1 = 0, p2 = 0;
+            uint32_t l = ~0u;
+            int src = -1, okd = ok ? 1 : -1;
+            if (ok) {
+                // the least key over this lane's records (branch-free), then the wave's
+                uint64_t mh = ~0ull;
+                uint32_t mphys = 0;
+                int mw = -1, cnt = 0;
+#pragma unroll
+                for (int p = 0; p < kPer; p++) {
+                    const int w = lane + 64 * p;
+                    const uint64_t hh = w < nwg ? lo64(rec[p][0]) : ~0ull;
+                    const bool lt = hh < mh, eq = hh == mh;
+                    cnt = lt ? 1 : (eq ? cnt + 1 : cnt);
+                    mw = lt ? w : mw;
+                    mphys = lt ? rec[p][0].z : mphys;
+                    mh = lt ? hh : mh;
+                }
+                hmin = wave_min_u64(mh);
+                const bool has = hmin != ~0ull && mh == hmin;
+                const unsigned long long bal = __ballot(has);
+                const bool tie = (__ballot(has && cnt > 1) != 0ull) || __popcll(bal) > 1;
+                if (hmin == ~0ull) {
+                    okd = 0;                            // no eligible column: OPTIMAL
+                } else if (!tie) {
+                    const int wl = __ffsll((long long)bal) - 1;
+                    src = (int)rdl32((uint32_t)mw, wl);
+                    p1 = rdl32(mphys, wl);
+                    if (lane == 0) g1 = rec_load(recP, (nwg + src) * 16);   // checked after the barrier
+                    g1src = src;
+                } else {
+                    // several records share the least key: j decides; fetch {P_q, j}
+                    // of each (bounded polls), the least j wins
+                    uint32_t bj = ~0u, bphys = 0;
+                    uint64_t bpq = 0;
+                    int bw = -1;
+                    const long long t0 = (long long)wall_clock64();
+#pragma unroll
+                    for (int p = 0; p < kPer; p++) {
+                        const int w = lane + 64 * p;
+                        if (w < nwg && lo64(rec[p][0]) == hmin) {
+                            u4 v = rec_load(recP, (nwg + w) * 16);
+                            while (v.w != tag && (long long)wall_clock64() - t0 <= kSpinTicks) {
+                                __builtin_amdgcn_s_sleep(1);
+                                v = rec_load(recP, (nwg + w) * 16);
+                            }
+                            if (v.w != tag) okd = -1;
+                            const bool better = v.z < bj;
+                            bj = better ? v.z : bj;
+                            bphys = better ? rec[p][0].z : bphys;
+                            bpq = better ? lo64(v) : bpq;
+                            bw = better ? w : bw;
+                        }
+                    }
+                    okd = __ballot(okd < 0) ? -1 : okd;
+                    const uint32_t jm = wave_min_u32(bj);
+                    const int wl = winner_lane(bw >= 0 && bj == jm);
+                    src = wl < 0 ? -1 : (int)rdl32((uint32_t)bw, wl);
+                    p1 = wl < 0 ? 0 : rdl32(bphys, wl);
+                    p2 = wl < 0 ? 0 : rdl64(bpq, wl);
+                    l = jm;
+                }
+                if (lane == 0) bc.z = lo64(xg);
+            }
+            if (lane == 0) {
+                bc.h = hmin;
+                bc.l = l;
+                bc.ok = okd < 0 ? -1 : (okd == 0 ? 0 : (src >= 0 ? 1 : -1));
+                bc.p0 = (1ull << 63) | (~hmin & 0x7fffffffffffffffull);   // dR at the entering column
+                bc.p1 = p1;
+                bc.p2 = p2;
+                bc.p3 = 0;
+            }
+        }
+        if (wave == 0 && !PK1) {
             u4 rec[kPer][NGP], pay[NGP - 1], xg{0u, 0u, 0u, 0u};
-            const bool ok = sweep<NGP, true>(recP, nwg, tag, rec, 2, st, &xg);
+            const bool ok = sweep<NGP, true>(recP, nwg, tag, rec, 2, st, &xg, xidx);
             uint64_t h = ~0ull, p0 = 0, p1 = 0, p2 = 0, p3 = 0;
             uint32_t l = ~0u;
             int src = -1;
@@ -901,13 +997,38 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         }
         __syncthreads();
         LPG_BPH(t, 4);
-        const int okS = bc.ok;
-        const int64_t kn = (int64_t)bc.l;               // logical entering column of pivot t + 1
-        const int64_t kp = (int64_t)bc.p1;              // its physical column
+        int okS = bc.ok;
+        const int64_t kp = (int64_t)bc.p1;              // physical column of the entering column
         const double nR = __longlong_as_double((long long)bc.p0), nM = __longlong_as_double((long long)bc.p3);
-        const double pkq = __longlong_as_double((long long)bc.p2);
         p0q = __longlong_as_double((long long)bc.z);
+        // column k's base entries on this slice's rows (HBM) and P_u[k] for
+        // u < q (Pbuf): in flight across the barrier below
+        double xa = (okS > 0 && hr) ? g.T[i * g.ld + kp] : 0.0;
+        double pu = (okS > 0 && wave * 64 < rw && lane < q) ? ld_wt(D.Pbuf + (int64_t)lane * g.ld + kp) : 0.0;
+        if (PK1 && wave == 0 && g1src >= 0) {
+            // the winner's {P_q[k], j}: stored with its key, so normally visible
+            if (lane == 0) {
+                const long long t0 = (long long)wall_clock64();
+                while (g1.w != tag && (long long)wall_clock64() - t0 <= kSpinTicks) {
+                    __builtin_amdgcn_s_sleep(1);
+                    g1 = rec_load(recP, (nwg + g1src) * 16);
+                }
+                if (g1.w != tag) {
+                    bc.ok = -1;
+                    st->stall_info[0] = 8;
+                    st->stall_info[1] = tag;
+                    st->stall_info[2] = nwg + g1src;
+                    st->stall_info[3] = g1.w;
+                } else {
+                    bc.l = g1.z;
+                    bc.p2 = lo64(g1);
+                }
+            }
+        }
         __syncthreads();
+        okS = bc.ok;
+        const int64_t kn = (int64_t)bc.l;               // logical entering column of pivot t + 1
+        const double pkq = __longlong_as_double((long long)bc.p2);   // P_q at the entering column
         const int s1 = s ^ 1;
         if (okS <= 0) {
             if (wg == 0 && tid == 0) {
@@ -926,9 +1047,8 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         }
         // column k of the current tableau; P_u[k] (lane u < q from Pbuf, P_q[k]
         // from the record; +0 past q)
-        double xa = hr ? g.T[i * g.ld + kp] : 0.0;
         if (wave * 64 < rw)                             // waves holding rows
-            wp[wave][lane] = lane < q ? ld_wt(D.Pbuf + (int64_t)lane * g.ld + kp) : (lane == q ? pkq : 0.0);
+            wp[wave][lane] = lane == q ? pkq : pu;
         LPG_BPH(t, 6);
         if (hr) b = (i == rl) ? p0q : fma(-sCt[q], p0q, b);
         // the chain over slots v <= q (NS > q). A row pivoted earlier in this
