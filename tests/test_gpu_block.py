@@ -227,3 +227,35 @@ def test_numeric_rule_matches_oracle(lpg, monkeypatch, persist, case):
     res = e.solve(1000, 0)
     assert res.status == ores.status and res.pivots == ores.pivots
     assert _log(e) == _log(o2)
+
+
+def _tied_lp(m, n, seed):
+    """A <= LP whose objective and coefficients take few distinct values
+    (quarters), so many columns share the least reduced cost exactly: the
+    pricing sweep's key ties (one-granule records, resolved by j) are hit at
+    the first pivots and again wherever the quantised entries repeat."""
+    rng = np.random.default_rng(seed)
+    T = np.zeros((m + 1, n + m + 1))
+    T[:m, 0] = 4.0 + rng.integers(0, 8, m)
+    T[:m, 1:n + 1] = rng.integers(1, 5, (m, n)) / 4.0
+    T[np.arange(m), n + 1 + np.arange(m)] = 1.0
+    T[m, 1:n + 1] = -(1.0 + rng.integers(0, 2, n) / 4.0)
+    return T, n + 1 + np.arange(m, dtype=np.int64)
+
+
+@pytest.mark.parametrize("wg", [None, 7])
+@pytest.mark.parametrize("defer", [32, 64])
+@pytest.mark.parametrize("m,n,seed", [(300, 500, 3), (97, 1500, 4)])
+def test_pricing_key_ties(lpg, monkeypatch, wg, defer, m, n, seed):
+    T, basis = _tied_lp(m, n, seed)
+    assert _fits(m, n + m + 1, defer, wg)
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer, wg=wg)
+    assert e.info.pivot_wg > 0
+    e.load_rows(0, T)
+    e.set_basis(basis)
+    o = Oracle(m, n + m + 1)
+    o.load_tableau(T, basis)
+    res = e.solve(3000, 0)
+    ores = o.solve(3000, 0)
+    assert res.status == ores.status and res.pivots == ores.pivots > 0
+    _assert_same(e, o, m)
