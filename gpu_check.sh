@@ -15,7 +15,6 @@ else
   rc=0
 fi
 timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
-if [ -n "${PROFILE:-}" ]; then ./tools/profile.sh || exit $?; fi
 for o in ${LATE_ORDERS:-}; do
   timeout -k 10 120 python tools/runtime_order.py $o >> gpurun_out/runtime_order.log 2>&1 || { echo "$o rc=$?" >> gpurun_out/runtime_order.log; exit 3; }
 done
