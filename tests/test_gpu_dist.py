@@ -263,7 +263,7 @@ def test_processes_two_phase_bitwise(lpg, world, m, n, rule, seed, lp, push, mr)
                                                   pytest.param(3, 700, 500, 7, "32", marks=pytest.mark.xfail(
                                                       strict=False, reason="open (DESIGN.md §5, end of round 3): in the "
                                                       "full GPU suite only, the last column's objective entry of "
-                                                      "this case differed from the oracle's in 2 of 3 runs (log and "
+                                                      "this case differed from the oracle's in 2 of 8 runs (log and "
                                                       "basis equal); alone it passes")),
                                                   (2, 1000, 800, 3, "128")])
 def test_processes_dual_bitwise(lpg, world, m, n, seed, defer):
