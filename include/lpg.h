@@ -30,9 +30,13 @@
  * Multi-GPU: one process per GPU. Each rank creates its context with
  * lpg_create_dist() and owns the row block [row0, row0 + nrows) of the m
  * constraint rows (row0 = floor(m*rank/world)); the objective row and the
- * basis are replicated. Per pivot the ranks exchange, over RCCL/xGMI, the
- * ratio-test candidates (allgather) and the normalised pivot row (allreduce
- * of the owner's row and zeros = broadcast from a device-resident root).
+ * basis are replicated. Per pivot the ranks exchange the ratio-test
+ * candidates and the normalised pivot row. Default for world > 1 (round 3):
+ * the owner push (lpg_comm_init_push*: the owner stores the row straight into
+ * every rank's IPC-mapped buffer over xGMI, flag per chunk). With a
+ * communicator only (or env LPG_EXCHANGE=rccl): RCCL collectives, an
+ * allgather of the candidates and an allreduce of the owner's row and zeros
+ * (= a broadcast from a device-resident root).
  */
 #ifndef LPG_H
 #define LPG_H
@@ -79,7 +83,7 @@ extern "C" {
 #define LPG_FLAG_EAGER   0x8u  /* one rank-1 update pass per pivot instead of deferred (blocked) updates */
 
 /* Deferred updates (default): the constraint rows are brought up to date in
- * one HBM pass per block of up to LPG_DEFER_MAX pivots (128 when a rank's
+ * one HBM pass per block of up to LPG_DEFER_MAX pivots (96 when a rank's
  * tableau is >= 16 GB, 64 when >= 200 MB, else 32; env LPG_DEFER=K picks K,
  * K in 1 .. 128; 0 = eager; the persistent pivot kernel takes blocks of at
  * most 64). Values,

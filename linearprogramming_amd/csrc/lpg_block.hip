@@ -507,8 +507,11 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         __syncthreads();
         if (!go) {
             if (tid == 0) {               // every workgroup alike: no pivot ran; the loop stops until the host
-                st->slot[0].status = ITER_LIMIT;   // has switched to the pair (lpg_ctx.hip recover_residency)
-                st->slot[1].status = ITER_LIMIT;
+                // has switched to the pair (lpg_ctx.hip recover_residency). Only a
+                // RUNNING slot is stopped: a terminal status (a launch enqueued
+                // after the loop had ended) is the result and stays
+                for (int u = 0; u < 2; u++)
+                    if (st->slot[u].status == RUNNING) st->slot[u].status = ITER_LIMIT;
                 st->stall = kStallResidency;
             }
             return;

@@ -113,6 +113,10 @@ struct lpg_ctx {
     int64_t cs = 0;
     int64_t *rq = nullptr;
     int skip = 1;                 // column skipping in the update (LPG_FLAG_NO_SKIP turns it off)
+    // tests only (LPG_TEST_PENDING_FAULT=F:W): before flush F, make the pending
+    // block inconsistent (W = npend | kq | lv | rq) to exercise k_swap_plan's guard
+    int inject_flush = -1, inject_what = 0;
+    int64_t nflush = 0;           // flush_launch calls so far
     unsigned long long touched_mark = 0;
     // communication
     ncclComm_t nccl = nullptr;
@@ -327,10 +331,25 @@ static bool reorders(const lpg_ctx *c) { return c->defer_k > 0 && c->fast_pivot 
 // The timing ring brackets the block pass alone (k_flushw / k_flushm), the
 // kernel the roofline reports; the swap plan, pivot-row rewrite and column
 // swaps around it count as "other" time per pivot.
+// The test hook's corruptions, one hipMemsetAsync each: npend = 0x7f7f.. (far
+// above any block), kq[0] = lv[0] = -1 (no column), rq[0] = 0x7f7f.. (no row).
+static int inject_pending_fault(lpg_ctx *c) {
+    switch (c->inject_what) {
+        case 1: HIPCHK(c, hipMemsetAsync(&c->st->npend, 0x7f, sizeof(int64_t), c->stream)); break;
+        case 2: HIPCHK(c, hipMemsetAsync(c->kq, 0xff, sizeof(int64_t), c->stream)); break;
+        case 3: HIPCHK(c, hipMemsetAsync(c->lv, 0xff, sizeof(int64_t), c->stream)); break;
+        case 4: HIPCHK(c, hipMemsetAsync(c->rq, 0x7f, sizeof(int64_t), c->stream)); break;
+        default: break;
+    }
+    return 0;
+}
+
 static int flush_launch(lpg_ctx *c) {
     int rc;
     const bool re = reorders(c);
-    if (launch_swap_plan(lau(c), c->st, defer_of(c, 0), c->colmap, c->inv, c->pairs, re ? 1 : 0) ||
+    if (c->inject_flush >= 0 && c->nflush == c->inject_flush && (rc = inject_pending_fault(c))) return rc;
+    c->nflush++;
+    if (launch_swap_plan(lau(c), geo(c), c->st, defer_of(c, 0), c->colmap, c->inv, c->pairs, re ? 1 : 0, c->defer_k) ||
         (re && launch_move_cols(lau(c), geo(c), c->st, defer_of(c, 0), c->pairs)))
         return fail(c, LPG_ERR_DEVICE, "swap plan launch failed");
     if (c->timing && ((rc = timing_mark(c, 0)) || (rc = timing_mark(c, 1)))) return rc;
@@ -701,6 +720,17 @@ static int recover_residency(lpg_ctx *c, const DevState &h) {
     return 0;
 }
 
+// k_swap_plan refused the pending block (lpg_kernels.hip): the loop was
+// stopped with NUMERIC and nothing of the block was applied.
+static int pending_fault(lpg_ctx *c, const DevState &h) {
+    static const char *const what[] = {"?", "npend", "kq", "lv", "rq"};
+    const int64_t w = h.stall_info[0] >= 1 && h.stall_info[0] <= 4 ? h.stall_info[0] : 0;
+    return fail(c, LPG_ERR_STATE,
+                "pending block inconsistent at the flush (%s[%lld] = %lld, npend %lld): the loop was stopped with "
+                "NUMERIC instead of indexing with it; the constraint rows were not brought up to date",
+                what[w], (long long)h.stall_info[1], (long long)h.stall_info[2], (long long)h.stall_info[3]);
+}
+
 static int read_result(lpg_ctx *c, lpg_result *out, int rule) {
     DevState h;
     HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));
@@ -712,6 +742,7 @@ static int read_result(lpg_ctx *c, lpg_result *out, int rule) {
         if (rc) return rc;
         h.stall = 0;
     }
+    if (h.stall == kStallPending) return pending_fault(c, h);
     if (h.stall == 2 || h.stall == 3)
         return fail(c, LPG_ERR_COMM, "owner-push exchange: rank %d waited > 2 s for the %s (a rank stopped, or the "
                     "buffers are not shared; LPG_EXCHANGE=rccl keeps the collectives)", c->rank,
@@ -854,6 +885,16 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->no_reorder = nr ? atoi(nr) != 0 : (world == 1 && tbytes < 2e9);
     const char *sp = getenv("LPG_SLOW_PIVOT");
     c->fast_pivot = !(sp && atoi(sp));
+    if (const char *pf = getenv("LPG_TEST_PENDING_FAULT")) {
+        char w[16] = {0};
+        int f = -1;
+        if (sscanf(pf, "%d:%15s", &f, w) == 2) {
+            static const char *const names[] = {"", "npend", "kq", "lv", "rq"};
+            for (int u = 1; u <= 4; u++)
+                if (!strcmp(w, names[u])) c->inject_what = u;
+            c->inject_flush = c->inject_what ? f : -1;
+        }
+    }
     const char *fv = getenv("LPG_FLUSH_KERNEL");   // m | w: force k_flushm / k_flushw (tests); default by block size
     c->flush_variant = fv ? (fv[0] == 'w' ? 1 : fv[0] == 'm' ? 0 : -1) : -1;
     int rc;
@@ -940,6 +981,12 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         (c->Cbuf && hipMemset(c->Cbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->cs * sizeof(double)) != hipSuccess) ||
         (c->Pbuf && hipMemset(c->Pbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->ld * sizeof(double)) != hipSuccess) ||
         (c->zrow && hipMemset(c->zrow, 0, (size_t)c->ld * sizeof(double)) != hipSuccess) ||
+        // slots a stopped block never filled read as out of range (kq = lv = 0,
+        // rq = -1 is a non-owner row), which k_swap_plan refuses
+        (c->kq && hipMemset(c->kq, 0, (size_t)flush_kmax_supported(c->defer_k) * sizeof(int64_t)) != hipSuccess) ||
+        (c->lv && hipMemset(c->lv, 0, (size_t)flush_kmax_supported(c->defer_k) * sizeof(int64_t)) != hipSuccess) ||
+        (c->rq && hipMemset(c->rq, 0xff, (size_t)flush_kmax_supported(c->defer_k) * sizeof(int64_t)) != hipSuccess) ||
+        (c->pv && hipMemset(c->pv, 0, (size_t)flush_kmax_supported(c->defer_k) * sizeof(double)) != hipSuccess) ||
         (c->rec && hipMemset(c->rec, 0, (size_t)block_records_bytes(c->pb_nwg)) != hipSuccess) ||
         (c->colmap && (launch_iota(lau(c), c->colmap, c->ld) || launch_iota(lau(c), c->inv, c->ld)))) {
         fail(c, LPG_ERR_DEVICE, "hipMemset failed");
@@ -1522,7 +1569,13 @@ static int solve_dual_deferred(lpg_ctx *c, int64_t max_pivots, lpg_result *out) 
     if (launch_dual_rows(L, g, c->drc, nrc)) return fail(c, LPG_ERR_DEVICE, "dual rows launch failed");
     c->par = 0;
     c->booted = false;
-    const bool keep = c->no_reorder;
+    // the column trade stays off for the dual's whole run and comes back on
+    // every exit, the HIPCHK early returns included
+    struct ReorderGuard {
+        lpg_ctx *c;
+        bool keep;
+        ~ReorderGuard() { c->no_reorder = keep; }
+    } guard{c, c->no_reorder};
     c->no_reorder = true;
     int rc = 0;
     // one pivot: (MR: every rank's row candidates) row_d, (MR: R summed over
@@ -1559,6 +1612,7 @@ static int solve_dual_deferred(lpg_ctx *c, int64_t max_pivots, lpg_result *out) 
         DevState h;
         HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (h.stall == kStallPending) return pending_fault(c, h);
         if (h.slot[c->par].status != LPG_RUNNING) break;
         batch = std::min<int64_t>(batch * 2, 256);
     }
@@ -1566,16 +1620,18 @@ static int solve_dual_deferred(lpg_ctx *c, int64_t max_pivots, lpg_result *out) 
     if (!rc && hipMemsetAsync(&c->st->slot[c->par].dpend, 0, sizeof(int64_t), c->stream) != hipSuccess)
         rc = fail(c, LPG_ERR_DEVICE, "hipMemsetAsync failed");
     if (!rc) rc = materialize(c);
-    c->no_reorder = keep;
     if (rc) return rc;
     DevState h;
     double z = 0;
     HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(&z, c->T + (c->nloc + c->nobj - 1) * c->ld, sizeof z, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (h.stall == kStallPending) return pending_fault(c, h);
     const int32_t st = h.slot[c->par].status;
     lpg_result r;
-    r.status = st == LPG_RUNNING ? LPG_ITER_LIMIT : st;
+    // the final row-only k_dual_row_d publishes its optimality peek as r = -1
+    // on a RUNNING slot (it never writes the status its own blocks read)
+    r.status = st != LPG_RUNNING ? st : h.slot[c->par].r < 0 ? LPG_OPTIMAL : LPG_ITER_LIMIT;
     r.rule = LPG_RULE_DANTZIG;
     r.pivots = h.pivots;
     r.objective = z;
@@ -1623,6 +1679,7 @@ int lpg_solve_dual(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
         DevState h;
         HIPCHK(c, hipMemcpyAsync(&h, c->st, sizeof h, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (h.stall == kStallPending) return pending_fault(c, h);
         if (h.slot[c->par].status != LPG_RUNNING) break;
         batch = std::min<int64_t>(batch * 2, 256);
     }

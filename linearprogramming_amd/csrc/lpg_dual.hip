@@ -115,11 +115,14 @@ __global__ __launch_bounds__(256) void k_dual_row_d(double *__restrict__ T, Geo 
         if (col) *(d2 *)(T + rR * g.ld + 2 * j2) = d;
     }
     best = block_reduce_cand(best);
-    if (best.row < 0) {                      // primal feasible: optimal
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            st->slot[s].status = OPTIMAL;
-            st->slot[s].r = -1;
-        }
+    // Primal feasible: optimal. Only r = -1 is published here, never the
+    // status: every block of this launch reads slot[s].status on entry, and a
+    // block scheduled after block 0 had written OPTIMAL there would return
+    // without the owed update above (the round-3 stale objective column).
+    // k_dual_col_d (or the host, after the final row-only launch) turns
+    // RUNNING with r < 0 into OPTIMAL.
+    if (best.row < 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) st->slot[s].r = -1;
         r_identity();
         return;
     }
@@ -260,9 +263,11 @@ __global__ __launch_bounds__(256) void k_dual_col_d(const double *__restrict__ T
     const double p0l1 = lq1 ? D.Pbuf[(int64_t)(64 + lane) * g.ld] : 0.0;
     const uint32_t rql1 = lq1 ? (uint32_t)D.rq[64 + lane] : 0xffffffffu;
     Slot *dst = &st->slot[s1];
-    if (stt != RUNNING) {
+    if (stt != RUNNING || r < 0) {           // r < 0 while RUNNING: row_d found the basis optimal
         if (blockIdx.x == 0 && threadIdx.x == 0) {
-            dst->status = stt;
+            const int32_t sv = stt != RUNNING ? stt : OPTIMAL;
+            st->slot[s].status = sv;         // every block of this launch returns here, whichever it reads
+            dst->status = sv;
             dst->k = -1;
             dst->r = -1;
             dst->dpend = 0;

@@ -52,12 +52,14 @@ struct DevState {
     int64_t npend;                // deferred pivots applied but not yet flushed (prep_t sets q + 1)
     unsigned long long fwork;     // k_flush work-item dequeue head (reset with npend after each flush)
     int64_t stall;                // set by k_pivot_block when a workgroup gave up waiting (lpg_block.hip);
-                                  // kStallResidency: a launch found its grid not co-resident and did nothing
+                                  // kStallResidency: a launch found its grid not co-resident and did nothing;
+                                  // kStallPending: k_swap_plan found the pending block inconsistent
     int64_t stall_info[4];        // its view then: phase (1 P, 2 S), expected tag, record index, tag seen
     uint32_t rcnt;                // k_pivot_block residency census: arrivals (launch L's count from L * nwg)
     uint32_t rdec;                // its decision word: (L << 2) | kGo / kAbort (single rank)
 };
 constexpr int64_t kStallResidency = 4;
+constexpr int64_t kStallPending = 5;
 
 // Pending-pivot buffers of the deferred update (Defer::on == 0: eager mode).
 struct Defer {
@@ -213,8 +215,10 @@ int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0:
 // pass) moves the leaving columns' data and P entries into place;
 // launch_fill_cols (after the pivot-row rewrite) writes the entering
 // columns' unit vectors (lpg_kernels.hip, above k_swap_plan).
-int launch_swap_plan(const Launch &L, const DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
-                     int32_t *pairs, int plan);   // reads D.pv (replicated pivot elements)
+// kmax: the pending block's bound (npend above it, or a slot's kq / lv / rq
+// out of range, stops the loop with kStallPending instead of indexing).
+int launch_swap_plan(const Launch &L, const Geo &g, DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
+                     int32_t *pairs, int plan, int kmax);   // reads D.pv (replicated pivot elements)
 int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs);
 // st != nullptr: also clears the pending block (npend, fwork), in place of
 // launch_flush_tail's memset (one dispatch fewer per block)

@@ -2095,13 +2095,58 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
 // mul[u][q] = -C_u[r_q] for u > q (+0 elsewhere), rows of LPG_DEFER_MAX.
 constexpr int kMulBlocks = 8;
 constexpr int kPlanNT = LPG_DEFER_MAX;                     // one thread per event / slot
-__global__ __launch_bounds__(kPlanNT) void k_swap_plan(const DevState *__restrict__ st, const int64_t *__restrict__ kq,
+//
+// Every block first checks the pending block it is about to index with: npend
+// within [0, kmax], and for each pending pivot q: rq[q] a local row in
+// [-1, nloc) and, with a plan, kq[q] and lv[q] logical columns in [1, ncols). A block stopped
+// mid-way (a stall, a give-up of the owner push) can leave npend ahead of the
+// slots it filled. On a violation no block writes anything it indexes with
+// those values; block 0 empties the pending block (npend = 0, pairs[0] = 0:
+// every flush kernel after this one is a no-op), stops a RUNNING loop with
+// NUMERIC and records kStallPending (lpg_last_error names it). Blocks that
+// read npend after block 0 cleared it see an empty block: the same outcome.
+__global__ __launch_bounds__(kPlanNT) void k_swap_plan(DevState *__restrict__ st, const int64_t *__restrict__ kq,
                                                   const int64_t *__restrict__ lv, const int64_t *__restrict__ rq,
                                                   const double *__restrict__ Cbuf, int64_t cs,
                                                   int32_t *__restrict__ colmap, int32_t *__restrict__ inv,
                                                   int32_t *__restrict__ pairs, double *__restrict__ mul, int plan,
-                                                  const double *__restrict__ pv) {
-    const int np = (int)st->npend;
+                                                  const double *__restrict__ pv, int64_t nloc, int64_t ncols, int kmax) {
+    const int64_t np64 = st->npend;
+    const bool npbad = np64 < 0 || np64 > kmax;
+    const int np = npbad ? 0 : (int)np64;
+    {
+        const int q = threadIdx.x;
+        int what = npbad ? 1 : 0;
+        int64_t val = np64;
+        if (!npbad && q < np) {
+            // kq / lv only feed the column plan (the generic deferred k_prep
+            // records neither, and runs without one)
+            const int64_t x = plan ? kq[q] : 1, y = plan ? lv[q] : 1, r = rq[q];
+            if (x < 1 || x >= ncols) what = 2, val = x;
+            else if (y < 1 || y >= ncols) what = 3, val = y;
+            else if (r < -1 || r >= nloc) what = 4, val = r;
+        }
+        __shared__ int first;
+        if (q == 0) first = kPlanNT;
+        __syncthreads();
+        if (what) atomicMin(&first, q);
+        if (__syncthreads_or(what != 0)) {
+            if (blockIdx.x == 0 && q == first) {
+                if (st->stall == 0) {       // a stall already recorded (the cause, e.g. an exchange give-up) is kept
+                    st->stall_info[0] = what;   // 1 npend, 2 kq, 3 lv, 4 rq
+                    st->stall_info[1] = q;
+                    st->stall_info[2] = val;
+                    st->stall_info[3] = np64;
+                    st->stall = kStallPending;
+                }
+                st->npend = 0;
+                if (pairs) pairs[0] = 0;
+                for (int u = 0; u < 2; u++)
+                    if (st->slot[u].status == RUNNING) st->slot[u].status = NUMERIC;
+            }
+            return;
+        }
+    }
     if (blockIdx.x > 0) {                                   // mul[u][q], lane q
         constexpr int UB = LPG_DEFER_MAX / kMulBlocks;       // pivots u per block
         const int q = threadIdx.x;
@@ -2251,10 +2296,12 @@ __global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Ge
         row[pairs[2 + 3 * p]] = (i == (int64_t)pairs[3 + 3 * p]) ? 1.0 : 0.0;
 }
 
-int launch_swap_plan(const Launch &L, const DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
-                     int32_t *pairs, int plan) {
+int launch_swap_plan(const Launch &L, const Geo &g, DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
+                     int32_t *pairs, int plan, int kmax) {
+    kmax = flush_kmax_supported(kmax);
+    if (!kmax || (plan && !pairs)) return -1;
     hipLaunchKernelGGL(k_swap_plan, dim3(1 + kMulBlocks), dim3(kPlanNT), 0, (hipStream_t)L.stream, st, D.kq, D.lv, D.rq,
-                       D.Cbuf, D.cs, colmap, inv, pairs, D.mul, plan, D.pv);
+                       D.Cbuf, D.cs, colmap, inv, pairs, D.mul, plan, D.pv, g.nloc, g.ncols, kmax);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2331,7 +2378,7 @@ int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &
 }
 
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant) {
-    int rc = launch_swap_plan(L, st, D, nullptr, nullptr, nullptr, 0);   // the multipliers only
+    int rc = launch_swap_plan(L, g, st, D, nullptr, nullptr, nullptr, 0, kmax);   // the multipliers only
     if (!rc) rc = launch_flush_main(L, g, st, D, kmax, skip, variant);
     return rc ? rc : launch_flush_tail(L, g, st, D, kmax);
 }

@@ -133,6 +133,37 @@ def test_gpu_dual_deferred_full_size(lpg):
 
 
 @pytest.mark.gpu
+def test_gpu_dual_optimal_with_late_workgroups(lpg):
+    """A dual LP whose rows span ~4900 column blocks of k_dual_row_d, far more
+    workgroups than the chip holds at once, so most start after workgroup 0
+    has finished. The round-3 kernel let workgroup 0 publish OPTIMAL into the
+    status word every workgroup reads on entry, and a late one then skipped
+    the objective row's owed update. This LP (230
+    pivots) reaches optimality mid-block with that update owed: status,
+    pivots, log, basis, the whole objective row and column 0 bitwise the
+    oracle's."""
+    m, n, seed = 32, 2_500_000, 11
+    e = lpg.Engine(m, n + m + 1)
+    assert e.info.defer_k == 64
+    e.generate(n, seed, lpg.GEN_DUAL)
+    r = e.solve_dual(100_000)
+    o = Oracle(m, n + m + 1, nthreads=min(16, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    o.generate(n, seed, GEN_DUAL)
+    ro = o.solve_dual(100_000)
+    assert r.status == ro.status == STATUS["OPTIMAL"] and r.pivots == ro.pivots and r.objective == ro.objective
+    assert 0 < ro.pivots % 64, "optimality must come mid-block (an owed update pending)"
+    ek, er = e.get_log()
+    ok, orr = o.get_log()
+    assert np.array_equal(ek, ok) and np.array_equal(er, orr)
+    assert np.array_equal(e.get_basis(), o.get_basis())
+    eo, oo = e.get_rows(m, 1)[0], o.get_rows(m, 1)[0]
+    bad = np.flatnonzero(eo.view(np.uint64) != oo.view(np.uint64))
+    assert bad.size == 0, f"objective row differs in {bad.size} columns, first {bad[:8].tolist()}"
+    assert np.array_equal(e.get_column0(), o.get_rows(0, m)[:, 0])
+    e.close()
+
+
+@pytest.mark.gpu
 def test_gpu_dual_infeasible_and_errors(lpg):
     T = np.array([[-2.0, -1, -1, 1, 0], [1.0, 1, 1, 0, 1], [0, 1, 1, 0, 0]])
     e = lpg.Engine(2, 5)

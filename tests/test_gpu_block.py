@@ -259,3 +259,32 @@ def test_pricing_key_ties(lpg, monkeypatch, wg, defer, m, n, seed):
     ores = o.solve(3000, 0)
     assert res.status == ores.status and res.pivots == ores.pivots > 0
     _assert_same(e, o, m)
+
+
+@pytest.mark.parametrize("persist", [None, 0])
+@pytest.mark.parametrize("what", ["npend", "kq", "lv", "rq"])
+def test_inconsistent_pending_block_stops_numeric(lpg, monkeypatch, what, persist):
+    """k_swap_plan's guard (a stopped block left npend
+    ahead of the slots it filled, and the plan indexed inv / colmap / Cbuf
+    with what it found, faulting the GPU). The test hook corrupts the pending
+    block before the second flush, with the column trade on: the loop stops
+    with NUMERIC, the flush applies nothing, lpg_last_error names the field --
+    and the GPU is healthy after it (a fresh engine solves bitwise)."""
+    m, n = 600, 1100
+    monkeypatch.setenv("LPG_TEST_PENDING_FAULT", f"1:{what}")
+    monkeypatch.setenv("LPG_NO_REORDER", "0")          # the column trade on: the plan indexes with kq / lv
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32, persist=persist)
+    monkeypatch.delenv("LPG_TEST_PENDING_FAULT")
+    assert e.info.column_trade == 1 and (e.info.pivot_wg > 0) == (persist is None)
+    e.generate(n, 5, 0)
+    with pytest.raises(lpg.LPGError, match=rf"pending block inconsistent at the flush \({what}\["):
+        e.solve(100_000, 0)
+    e.close()
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32, persist=persist)
+    e.generate(n, 5, 0)
+    res = e.solve(100_000, 0)
+    o = Oracle(m, n + m + 1)
+    o.generate(n, 5, 0)
+    ores = o.solve(100_000, 0)
+    assert res.status == ores.status == 1 and res.pivots == ores.pivots > 64
+    _assert_same(e, o, m)

@@ -260,11 +260,7 @@ def test_processes_two_phase_bitwise(lpg, world, m, n, rule, seed, lp, push, mr)
 
 
 @pytest.mark.parametrize("world,m,n,seed,defer", [(2, 100, 150, 3, None), (3, 400, 300, 3, None), (2, 257, 200, 5, "5"),
-                                                  pytest.param(3, 700, 500, 7, "32", marks=pytest.mark.xfail(
-                                                      strict=False, reason="open (DESIGN.md §5, end of round 3): in the "
-                                                      "full GPU suite only, the last column's objective entry of "
-                                                      "this case differed from the oracle's in 2 of 8 runs (log and "
-                                                      "basis equal); alone it passes")),
+                                                  (3, 700, 500, 7, "32"),
                                                   (2, 1000, 800, 3, "128")])
 def test_processes_dual_bitwise(lpg, world, m, n, seed, defer):
     """The deferred dual simplex over 2-3 processes (round 3; single rank
