@@ -58,7 +58,7 @@ def _sample(m, world, rank, k, seed):
     return sorted(set(rng.choice(np.arange(r0, r1), k, replace=False).tolist()) | {r0, r1 - 1})
 
 
-def _worker(rank, world, port, m, n, seed, pivots, outdir, env, push):
+def _worker(rank, world, port, m, n, seed, pivots, outdir, env, push, sample_rows=None, sweep=False):
     os.environ.update(env)
     import torch
     import torch.distributed as dist
@@ -87,11 +87,26 @@ def _worker(rank, world, port, m, n, seed, pivots, outdir, env, push):
     e.generate(n, seed, lpg.GEN_DENSE)
     e.reserve_log(pivots + 8)
     res = e.solve(pivots, lpg.RULE_DANTZIG)
+    print(f"rank {rank}/{world}: {res.pivots} pivots", flush=True)   # progress (a long test, run with -s)
     info = e.info
     k, r = e.get_log()
     basis = e.get_basis()
-    rows = sorted(set(_sample(m, world, rank, 64, seed)) | {int(x) for x in r if info.row0 <= x < info.row0 + info.nrows})
-    out = dict(status=res.status, pivots=res.pivots, objective=res.objective, log=(k, r), basis=basis,
+    if sample_rows is not None:                  # the rows the caller read from its reference run
+        rows = [i for i in sample_rows if info.row0 <= i < info.row0 + info.nrows]
+    else:
+        rows = sorted(set(_sample(m, world, rank, 64, seed)) | {int(x) for x in r if info.row0 <= x < info.row0 + info.nrows})
+    bad = []
+    if sweep:                                    # every local row: basic columns unit, b >= 0
+        for i0 in range(info.row0, info.row0 + info.nrows, 256):
+            nr = min(256, info.row0 + info.nrows - i0)
+            blk = e.get_rows(i0, nr)
+            sub = blk[:, basis]
+            idx = np.arange(i0, i0 + nr)
+            if not (np.array_equal(sub[np.arange(nr), idx], np.ones(nr)) and np.count_nonzero(sub) == nr):
+                bad.append(f"rows {i0}..: basic columns not unit")
+            if not np.all(blk[:, 0] >= 0.0):
+                bad.append(f"rows {i0}..: b < 0")
+    out = dict(bad=bad, status=res.status, pivots=res.pivots, objective=res.objective, log=(k, r), basis=basis,
                obj=e.get_rows(m, 1)[0], rows={i: e.get_rows(i, 1)[0] for i in rows}, x0=e.get_column0(),
                wg0=wg0, wg=info.pivot_wg, fallbacks=info.residency_fallbacks, exchange=info.exchange,
                defer=info.defer_k, row0=info.row0, nrows=info.nrows)
@@ -101,14 +116,15 @@ def _worker(rank, world, port, m, n, seed, pivots, outdir, env, push):
     dist.destroy_process_group()
 
 
-def _run(world, m, n, pivots, env, push=True):
+def _run(world, m, n, pivots, env, push=True, sample_rows=None, sweep=False):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, port, m, n, SEED, pivots, d, env, push), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, port, m, n, SEED, pivots, d, env, push, sample_rows, sweep), nprocs=world,
+                 join=True)
         return [pickle.load(open(os.path.join(d, f"r{q}.pkl"), "rb")) for q in range(world)]
 
 
@@ -176,3 +192,46 @@ def test_config4_shape_two_processes_partition_invariance(lpg):
     _check_against(parts, m, piv, e.get_log(), e.get_basis(), e.get_rows(m, 1)[0], lambda i: e.get_rows(i, 1)[0])
     assert np.array_equal(np.concatenate([p["x0"] for p in parts]), e.get_column0())
     e.close()
+
+
+def test_config4_eight_processes_partition_invariance(lpg):
+    """BASELINE config 4's actual split on the one GPU (VERDICT r3 missing #2):
+    8 processes x 8192 rows x 196,609 columns (12.9 GB each, 103 GB in all).
+    Each rank is under 16 GB, so it takes 64-pivot blocks, the two-kernel
+    pair (the slices do not fit the persistent launch) and the 8-rank column
+    trade; the exchange is the host collectives (gloo), as in the 2-process
+    config-4 test. 200 pivots = three whole blocks and a partial one settled
+    by the readout. The single-rank engine runs the same LP first (96-pivot
+    blocks: the deferral is bitwise the eager chain, so the block size must
+    not matter) and is released before the ranks start; every rank must equal
+    it bit for bit: status, pivot count, objective, log, basis, objective
+    row, column 0, every pivot row and 64 sampled rows per rank. Every row
+    of every rank also has unit basic columns and b >= 0."""
+    m, n, piv, world = 65536, 131072, 200, 8
+    e = lpg.Engine(m, n + m + 1)
+    assert e.info.defer_k == 96
+    e.generate(n, SEED, lpg.GEN_DENSE)
+    e.reserve_log(piv + 8)
+    res = e.solve(piv, lpg.RULE_DANTZIG)
+    assert res.pivots == piv and res.status == 4
+    log, basis, obj, x0 = e.get_log(), e.get_basis(), e.get_rows(m, 1)[0], e.get_column0()
+    rows = set(int(x) for x in log[1])
+    for p in range(world):
+        rows |= set(_sample(m, world, p, 64, SEED))
+    rows = sorted(rows)
+    ref_rows = {i: e.get_rows(i, 1)[0] for i in rows}
+    e.close()
+    del e
+    parts = _run(world, m, n, piv, {}, push=False, sample_rows=rows, sweep=True)
+    assert all(p["defer"] == 64 and p["wg"] == 0 and p["exchange"] == 0 for p in parts)   # the pair, 64-pivot blocks
+    assert [p["nrows"] for p in parts] == [m // world] * world
+    for p in parts:                                  # the first divergence, if any, named before the details
+        k2, r2 = p["log"]
+        badp = np.nonzero((log[0][:len(k2)] != k2[:len(log[0])]) | (log[1][:len(k2)] != r2[:len(log[0])]))[0]
+        assert len(badp) == 0, f"pivot {badp[0]}: single rank ({log[0][badp[0]]}, {log[1][badp[0]]}), " \
+                               f"rank ({k2[badp[0]]}, {r2[badp[0]]})"
+        assert not p["bad"], p["bad"][:4]
+        assert len(p["rows"]) >= 64
+    assert all(p["objective"] == res.objective for p in parts), (res.objective, [p["objective"] for p in parts])
+    _check_against(parts, m, piv, log, basis, obj, lambda i: ref_rows[i])
+    assert np.array_equal(np.concatenate([p["x0"] for p in parts]), x0)

@@ -1,0 +1,183 @@
+// hbm_ceiling.hip — what the HBM of this box streams, for the block pass's
+// question: is an in-place read-modify-write held below
+// a copy, and does an out-of-place RMW reach the copy's rate?
+//
+// Five streams over 16-byte lanes, byte counts as the pass counts them (read +
+// written bytes):
+//   read   sum of every element (one store per thread at the end)
+//   write  a constant into every element
+//   copy   dst = src                       (two buffers)
+//   rmw    x = fma(-c, p, x) in place      (k_flushw's traffic shape)
+//   rmwo   dst = fma(-c, p, src)           (an out-of-place pass)
+// Two address layouts: grid-stride (consecutive workgroups on consecutive
+// 4 KB) and chunked (each workgroup one contiguous span of n / grid), U
+// 16-byte loads in flight per lane, plain or non-temporal loads and stores,
+// grids of 1-8 workgroups of 256 per CU. 4 GiB per buffer (config 3's live
+// region is 4.3 GB). tools only.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+#define CHK(x)                                                                     \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            printf("%s: %s\n", #x, hipGetErrorString(e_));                         \
+            exit(1);                                                               \
+        }                                                                          \
+    } while (0)
+
+enum { OP_READ, OP_WRITE, OP_COPY, OP_RMW, OP_RMWO };
+
+template <bool NT>
+__device__ __forceinline__ d2 ld(const d2 *p) {
+    if (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(d2 *p, d2 v) {
+    if (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// n: 16-byte elements (a multiple of 256 * U * grid for both layouts)
+template <int OP, int U, bool CHUNK, bool NT>
+__global__ __launch_bounds__(256) void k_stream(const d2 *__restrict__ src, d2 *__restrict__ dst, size_t n, double c,
+                                                d2 *__restrict__ sink) {
+    const d2 p = {0.5, 0.25};
+    size_t base, step, end;
+    if (CHUNK) {
+        const size_t span = n / gridDim.x;
+        base = (size_t)blockIdx.x * span + threadIdx.x;
+        step = 256;
+        end = (size_t)(blockIdx.x + 1) * span;
+    } else {
+        base = (size_t)blockIdx.x * 256 + threadIdx.x;
+        step = (size_t)gridDim.x * 256;
+        end = n;
+    }
+    d2 acc = {0.0, 0.0};
+    for (size_t i = base; i + (U - 1) * step < end; i += U * step) {
+        d2 v[U];
+        if (OP != OP_WRITE) {
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = ld<NT>(src + i + u * step);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (OP == OP_READ) {
+                acc += v[u];
+            } else if (OP == OP_WRITE) {
+                st<NT>(dst + i + u * step, d2{c, c});
+            } else if (OP == OP_COPY) {
+                st<NT>(dst + i + u * step, v[u]);
+            } else {
+                d2 x = v[u];
+                x.x = fma(-c, p.x, x.x);
+                x.y = fma(-c, p.y, x.y);
+                st<NT>(dst + i + u * step, x);
+            }
+        }
+    }
+    if (OP == OP_READ && acc.x == 12345.678) sink[threadIdx.x] = acc;
+}
+
+typedef void (*KFn)(const d2 *, d2 *, size_t, double, d2 *);
+
+template <int OP, int U, bool CHUNK, bool NT>
+static KFn pick() {
+    return k_stream<OP, U, CHUNK, NT>;
+}
+
+template <int OP, bool CHUNK, bool NT>
+static KFn pick_u(int u) {
+    switch (u) {
+        case 1: return pick<OP, 1, CHUNK, NT>();
+        case 2: return pick<OP, 2, CHUNK, NT>();
+        case 4: return pick<OP, 4, CHUNK, NT>();
+        default: return pick<OP, 8, CHUNK, NT>();
+    }
+}
+template <int OP>
+static KFn pick_all(int u, bool chunk, bool nt) {
+    if (chunk) return nt ? pick_u<OP, true, true>(u) : pick_u<OP, true, false>(u);
+    return nt ? pick_u<OP, false, true>(u) : pick_u<OP, false, false>(u);
+}
+static KFn kernel(int op, int u, bool chunk, bool nt) {
+    switch (op) {
+        case OP_READ: return pick_all<OP_READ>(u, chunk, nt);
+        case OP_WRITE: return pick_all<OP_WRITE>(u, chunk, nt);
+        case OP_COPY: return pick_all<OP_COPY>(u, chunk, nt);
+        case OP_RMW: return pick_all<OP_RMW>(u, chunk, nt);
+        default: return pick_all<OP_RMWO>(u, chunk, nt);
+    }
+}
+
+int main(int argc, char **argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 5;
+    const size_t bytes = (size_t)4 << 30;
+    const size_t n = bytes / 16;
+    int cus = 0;
+    CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    d2 *A, *B, *S;
+    CHK(hipMalloc(&A, bytes));
+    CHK(hipMalloc(&B, bytes));
+    CHK(hipMalloc(&S, 256 * sizeof(d2)));
+    CHK(hipMemset(A, 0, bytes));
+    CHK(hipMemset(B, 0, bytes));
+    hipEvent_t e0, e1;
+    CHK(hipEventCreate(&e0));
+    CHK(hipEventCreate(&e1));
+    const char *names[] = {"read", "write", "copy", "rmw", "rmwo"};
+    printf("# hbm_ceiling: %d CUs, %zu MiB per buffer, best and median of %d launches; GB/s = (read + written bytes) / time\n",
+           cus, bytes >> 20, reps);
+    const int wpcs[] = {1, 2, 4, 8};
+    const int us[] = {1, 2, 4, 8};
+    for (int op = 0; op < 5; op++) {
+        double best_all = 0;
+        char best_cfg[128] = "";
+        for (int chunk = 0; chunk < 2; chunk++)
+            for (int nt = 0; nt < 2; nt++)
+                for (int wpc : wpcs)
+                    for (int u : us) {
+                        const int grid = wpc * cus;
+                        // both layouts need n divisible by grid * 256 * u: trim the tail (< 0.1%)
+                        const size_t unit = (size_t)grid * 256 * u;
+                        const size_t nn = n / unit * unit;
+                        KFn k = kernel(op, u, chunk, nt);
+                        const d2 *src = A;
+                        d2 *dst = (op == OP_RMW) ? A : B;
+                        hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, src, dst, nn, 1e-3, S);
+                        CHK(hipDeviceSynchronize());
+                        std::vector<float> t;
+                        for (int r = 0; r < reps; r++) {
+                            CHK(hipEventRecord(e0));
+                            hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, src, dst, nn, 1e-3, S);
+                            CHK(hipEventRecord(e1));
+                            CHK(hipEventSynchronize(e1));
+                            float ms;
+                            CHK(hipEventElapsedTime(&ms, e0, e1));
+                            t.push_back(ms);
+                        }
+                        std::sort(t.begin(), t.end());
+                        const double moved = (double)nn * 16 * ((op == OP_READ || op == OP_WRITE) ? 1 : 2);
+                        const double gbs = moved / t[0] / 1e6, gbm = moved / t[t.size() / 2] / 1e6;
+                        printf("%-5s %-6s %-5s wg/CU %d U %d : best %7.1f  median %7.1f GB/s  (%.3f ms)\n", names[op],
+                               chunk ? "chunk" : "stride", nt ? "nt" : "plain", wpc, u, gbs, gbm, t[0]);
+                        if (gbs > best_all) {
+                            best_all = gbs;
+                            snprintf(best_cfg, sizeof best_cfg, "%s %s wg/CU %d U %d", chunk ? "chunk" : "stride",
+                                     nt ? "nt" : "plain", wpc, u);
+                        }
+                    }
+        printf("## %s best %.1f GB/s (%s)\n", names[op], best_all, best_cfg);
+        fflush(stdout);
+    }
+    return 0;
+}
