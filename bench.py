@@ -80,6 +80,10 @@ def parse():
     ap.add_argument("--force-push", action="store_true", help="N=1: attach the owner-push exchange to a 1-rank "
                                                               "host communicator (times the push kernels)")
     ap.add_argument("--defer", type=int, default=None, help="pivots per deferred block (LPG_DEFER; 0 = eager updates)")
+    ap.add_argument("--shape", default=None,
+                    help="M,N: a labelled stand-in LP of M rows and N structural columns in place of --config's "
+                         "(e.g. one rank's row block of config 3 at P ranks: M = 16384/P, N = 49152 - M; never the "
+                         "headline line)")
     return ap.parse_args()
 
 
@@ -227,6 +231,10 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = CONFIGS[a.config]
     m, n = cfg["m"], cfg["n"]
+    if a.shape:                                        # a stand-in shape, labelled as such in the line
+        m, n = (int(x) for x in a.shape.split(","))
+        cfg = dict(m=m, n=n, name=f"STAND-IN (not a BASELINE config): dense LP m={m} n={n} fp64, generated like "
+                                  f"config {a.config}")
     ndev = lpg.device_count()
     if ndev < 1:
         raise SystemExit("no GPU visible")

@@ -88,6 +88,64 @@ __global__ __launch_bounds__(256) void k_stream(const d2 *__restrict__ src, d2 *
     if (OP == OP_READ && acc.x == 12345.678) sink[threadIdx.x] = acc;
 }
 
+
+// The block pass's access shape without its arithmetic: a row-major tableau
+// (config 3: 16384 rows, pitch 49216 doubles), the first `live` columns of
+// every row read and written in place, in items of TW columns x IR rows
+// (column tile fastest, like k_flushw's dequeue order), a 256-thread
+// workgroup covering 256 / (TW / 2) rows per access, U accesses in flight
+// per lane. Grid-stride over items (no dequeue).
+template <int TW, int U>
+__global__ __launch_bounds__(256) void k_tile_rmw(double *__restrict__ T, long ld, long rows, long live, long ir,
+                                                  double c) {
+    constexpr int LPR = TW / 2;                 // lanes per row (16 B each)
+    constexpr int RPA = 256 / LPR;              // rows per access
+    const d2 p = {0.5, 0.25};
+    const long ntiles = (live + TW - 1) / TW;
+    const long nitems = ntiles * ((rows + ir - 1) / ir);
+    const int lc = threadIdx.x % LPR, lr = threadIdx.x / LPR;
+    for (long item = blockIdx.x; item < nitems; item += gridDim.x) {
+        const long tile = item % ntiles, strip = item / ntiles;
+        const long c0 = tile * TW + 2 * lc;
+        const bool in = c0 + 1 < live;
+        const long r0 = strip * ir, r1 = r0 + ir < rows ? r0 + ir : rows;
+        for (long rb = r0; rb < r1; rb += RPA * U) {
+            d2 v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const long r = rb + lr + u * RPA;
+                v[u] = (in && r < r1) ? __builtin_nontemporal_load((const d2 *)(T + r * ld + c0)) : d2{0.0, 0.0};
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const long r = rb + lr + u * RPA;
+                d2 x = v[u];
+                x.x = fma(-c, p.x, x.x);
+                x.y = fma(-c, p.y, x.y);
+                if (in && r < r1) __builtin_nontemporal_store(x, (d2 *)(T + r * ld + c0));
+            }
+        }
+    }
+}
+
+typedef void (*TFn)(double *, long, long, long, long, double);
+template <int TW>
+static TFn tile_u(int u) {
+    switch (u) {
+        case 2: return k_tile_rmw<TW, 2>;
+        case 4: return k_tile_rmw<TW, 4>;
+        case 8: return k_tile_rmw<TW, 8>;
+        default: return k_tile_rmw<TW, 16>;
+    }
+}
+static TFn tile_kernel(int tw, int u) {
+    switch (tw) {
+        case 128: return tile_u<128>(u);
+        case 256: return tile_u<256>(u);
+        default: return tile_u<512>(u);
+    }
+}
+
 typedef void (*KFn)(const d2 *, d2 *, size_t, double, d2 *);
 
 template <int OP, int U, bool CHUNK, bool NT>
@@ -178,6 +236,47 @@ int main(int argc, char **argv) {
                     }
         printf("## %s best %.1f GB/s (%s)\n", names[op], best_all, best_cfg);
         fflush(stdout);
+    }
+    // the block pass's shape: config 3's tableau, its 32770 live columns
+    CHK(hipFree(A));
+    CHK(hipFree(B));
+    {
+        const long rows = 16384, ld = 49216, live = 32770;
+        double *T;
+        CHK(hipMalloc(&T, (size_t)(rows + 1) * ld * 8));
+        CHK(hipMemset(T, 0, (size_t)(rows + 1) * ld * 8));
+        const double moved = 16.0 * rows * live;
+        double best_all = 0;
+        char best_cfg[128] = "";
+        for (int tw : {128, 256, 512})
+            for (long ir : {64L, 512L, 16384L})
+                for (int wpc : {1, 2, 4, 8})
+                    for (int u : {2, 4, 8, 16}) {
+                        const int grid = wpc * cus;
+                        TFn k = tile_kernel(tw, u);
+                        hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, T, ld, rows, live, ir, 1e-3);
+                        CHK(hipDeviceSynchronize());
+                        std::vector<float> t;
+                        for (int r = 0; r < reps; r++) {
+                            CHK(hipEventRecord(e0));
+                            hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, T, ld, rows, live, ir, 1e-3);
+                            CHK(hipEventRecord(e1));
+                            CHK(hipEventSynchronize(e1));
+                            float ms;
+                            CHK(hipEventElapsedTime(&ms, e0, e1));
+                            t.push_back(ms);
+                        }
+                        std::sort(t.begin(), t.end());
+                        const double gbs = moved / t[0] / 1e6, gbm = moved / t[t.size() / 2] / 1e6;
+                        printf("tile  TW %3d rows/item %5ld wg/CU %d U %2d : best %7.1f  median %7.1f GB/s  (%.3f ms)\n",
+                               tw, ir, wpc, u, gbs, gbm, t[0]);
+                        if (gbs > best_all) {
+                            best_all = gbs;
+                            snprintf(best_cfg, sizeof best_cfg, "TW %d rows/item %ld wg/CU %d U %d", tw, ir, wpc, u);
+                        }
+                    }
+        printf("## tile best %.1f GB/s (%s)\n", best_all, best_cfg);
+        CHK(hipFree(T));
     }
     return 0;
 }
