@@ -203,6 +203,38 @@ int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, in
 int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which);
 // reset = false: the caller clears npend / fwork itself (launch_fill_cols with st)
 int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, bool reset = true);
+// Item map of the banded block pass (k_flushw): column tile
+// fastest, `rows`-row strips; when the rows hold >= 8 strips the last two are
+// cut into items of rows / 4 (a multiple of 16), so that the dynamic queue
+// ends on short items (the last round of whole items left most CUs idle while
+// a few finished theirs). flush_nitems is the host's count for the launch.
+// rows < 0: |rows|-row items throughout, no tail (LPG_FLUSH_TAIL=0, A/B)
+__host__ __device__ inline int64_t flush_tail_rows(int64_t rows, int64_t nloc) {
+    return (rows > 0 && nloc >= 8 * rows && rows >= 64) ? rows / 4 : 0;
+}
+__host__ __device__ inline int64_t flush_nitems(int64_t ntiles, int64_t rows, int64_t nloc) {
+    const int64_t tr = flush_tail_rows(rows, nloc);
+    if (rows < 0) rows = -rows;
+    if (!tr) return ntiles * ((nloc + rows - 1) / rows);
+    const int64_t t0 = ((nloc + rows - 1) / rows - 2) * rows;
+    return ntiles * (t0 / rows) + ntiles * ((nloc - t0 + tr - 1) / tr);
+}
+__host__ __device__ inline void flush_item(int64_t item, int64_t ntiles, int64_t rows, int64_t nloc, int64_t &tile,
+                                           int64_t &i0, int64_t &i1) {
+    const int64_t tr = flush_tail_rows(rows, nloc);
+    if (rows < 0) rows = -rows;
+    const int64_t t0 = tr ? ((nloc + rows - 1) / rows - 2) * rows : nloc;
+    const int64_t nbig = ntiles * (t0 / rows);
+    tile = item % ntiles;
+    if (!tr || item < nbig) {
+        i0 = (item / ntiles) * rows;
+        i1 = i0 + rows;
+    } else {
+        i0 = t0 + ((item - nbig) / ntiles) * tr;
+        i1 = i0 + tr;
+    }
+    if (i1 > nloc) i1 = nloc;
+}
 int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0: k too large)
 // Basis-partitioned column order (single-rank deferred path): after a block,
 // every column that went nonbasic -> basic during it swaps its physical

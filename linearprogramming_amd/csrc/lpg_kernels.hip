@@ -1857,9 +1857,8 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T,
         __syncthreads();
         const int64_t item = next_item;
         if (item >= nitems) break;
-        const int64_t tile = item % ntiles, strip = item / ntiles;
-        const int64_t i0 = strip * rows;
-        const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
+        int64_t tile, i0, i1;
+        flush_item(item, ntiles, rows, g.nloc, tile, i0, i1);
         const int64_t cl = tile * (32 * WPB) + wave * 32 + 2 * lc;   // this lane's column pair
         const bool in = cl < g.ncols;                                // cl even, ld even: cl + 1 < ld
         double be[G], bo[G];
@@ -2383,6 +2382,15 @@ int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, in
     return rc ? rc : launch_flush_tail(L, g, st, D, kmax);
 }
 
+// the short tail items of the banded passes (flush_item); LPG_FLUSH_TAIL=0 turns them off
+static bool flush_tail_on() {
+    static const int on = [] {
+        const char *v = getenv("LPG_FLUSH_TAIL");
+        return v ? atoi(v) != 0 : 1;
+    }();
+    return on != 0;
+}
+
 // which: -1 = default (k_flushw), 0 = k_flushm (blocks of <= 32 pivots),
 // 1 = k_flushw (LPG_FLUSH_KERNEL=m|w, tests). Both bitwise.
 int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which) {
@@ -2391,8 +2399,8 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
     // k_flushw by default at every block size: at 32 slots too it beats
     // k_flushm by 3-4% (m = 1024 .. 4096, profiles/r02_k32_flush.log)
     if (which < 0) which = 1;
-    if (kmax >= 64) which = 1;                              // k_flushm's C tile caps it at 32 slots
     hipStream_t stream = (hipStream_t)L.stream;
+    if (kmax >= 64) which = 1;                              // k_flushm's C tile caps it at 32 slots
     if (which == 1) {
         // k_flushw: 4-wave blocks, 128-column x 512-row items swept in 16-row
         // bands with a 2-deep LDS ring of multipliers; small tableaus shrink
@@ -2407,7 +2415,8 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
         // 128 rows 13% slower)
         int64_t rows = 512;
         while (rows > 64 && ntiles * ((g.nloc + rows - 1) / rows) < 2048) rows /= 2;
-        const int64_t nitems = ntiles * ((g.nloc + rows - 1) / rows);
+        if (!flush_tail_on()) rows = -rows;
+        const int64_t nitems = flush_nitems(ntiles, rows, g.nloc);
         const int lb = kmax == 128 ? 1 : kmax == 96 ? 2 : kmax == 64 ? 2 : 3;   // VGPRs: 184 at 64 slots, <= 128 below
         const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * lb);
         if (nblocks < 1) return 0;

@@ -24,6 +24,7 @@
         }                                                                           \
     } while (0)
 
+
 namespace lpg {
 
 template <int N>
@@ -31,7 +32,8 @@ __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// k_flushd: k_flushw's wave tile (16 rows x 32 columns, lane (lk, lc) holds
+// k_flushd (measured slower than k_flushw, not in the product: profiles/r04_flush64_lab.log):
+// k_flushw's wave tile (16 rows x 32 columns, lane (lk, lc) holds
 // column pair 2 lc and rows lk + 4 r; even / odd-column MFMA chains, B in
 // VGPRs) with the tableau band and the band's multipliers brought into an LDS
 // ring by LDS-DMA DT bands ahead. Per wave and band: 4 tableau DMAs (1 KB
@@ -51,7 +53,6 @@ __global__ __launch_bounds__(64 * WPB, 1) void k_flushd(double *__restrict__ T, 
                                                         const double *__restrict__ Cbuf, int64_t cs, int64_t ntiles,
                                                         int64_t nitems, int64_t rows, int skip,
                                                         const double *__restrict__ zrow, double *__restrict__ sink) {
-    constexpr int NTH = 64 * WPB;
     constexpr int G = KMAX / 4;
     constexpr int RING = DT + 1;
     constexpr int TWV = 512;                        // doubles of tableau per wave per band
@@ -76,9 +77,8 @@ __global__ __launch_bounds__(64 * WPB, 1) void k_flushd(double *__restrict__ T, 
         __syncthreads();
         const int64_t item = sx[0];
         if (item >= nitems) break;
-        const int64_t tile = item % ntiles, strip = item / ntiles;
-        const int64_t i0 = strip * rows;
-        const int64_t i1 = i0 + rows < g.nloc ? i0 + rows : g.nloc;
+        int64_t tile, i0, i1;
+        flush_item(item, ntiles, rows, g.nloc, tile, i0, i1);
         const int64_t cl = tile * (32 * WPB) + wave * 32 + 2 * lc;
         const bool in = cl < g.ncols;
         double be[G], bo[G];
@@ -171,6 +171,7 @@ constexpr size_t flushd_lds() {
     return (size_t)(DT + 1) * (WPB * 512 + 16 * KMAX) * sizeof(double) + (1 + WPB) * sizeof(int64_t);
 }
 
+
 }  // namespace lpg
 
 using namespace lpg;
@@ -215,11 +216,12 @@ struct Lab {
     }
 };
 typedef void (*LaunchFn)(Lab &L);
+static bool g_tail = true;   // the short tail items (flush_item); false: whole items throughout
 
 // the product's launch of k_flushw<64> (lpg_kernels.hip launch_flush_main)
 static void fn_ref(Lab &L) {
-    const int64_t tw = 256, ntiles = (L.g.ncols + tw - 1) / tw, rows = 512;
-    const int64_t nitems = ntiles * ((L.g.nloc + rows - 1) / rows);
+    const int64_t tw = 256, ntiles = (L.g.ncols + tw - 1) / tw, rows = g_tail ? 512 : -512;
+    const int64_t nitems = flush_nitems(ntiles, rows, L.g.nloc);
     const int64_t nblocks = std::min<int64_t>(nitems, 512);
     L.reset_state(64);
     hipLaunchKernelGGL((k_flushw<64, 2, 2, 8>), dim3((unsigned)((nblocks + 1) / 2)), dim3(512), 0, 0, L.g.T, L.g,
@@ -229,7 +231,8 @@ static void fn_ref(Lab &L) {
 template <int WPB, int DT, int R, int BPC>
 static void fn_d(Lab &L) {
     const int64_t tw = 32 * WPB, ntiles = (L.g.ncols + tw - 1) / tw;
-    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
+    const int64_t rows = g_tail ? R : -R;
+    const int64_t nitems = flush_nitems(ntiles, rows, L.g.nloc);
     const size_t lds = flushd_lds<64, WPB, DT>();
     static bool set = false;
     if (!set) {
@@ -239,7 +242,7 @@ static void fn_d(Lab &L) {
     }
     L.reset_state(64);
     hipLaunchKernelGGL((k_flushd<64, WPB, DT>), dim3((unsigned)std::min<int64_t>(nitems, 256 * BPC)), dim3(64 * WPB),
-                       lds, 0, L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, (int64_t)R, 1,
+                       lds, 0, L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, rows, 1,
                        (const double *)L.zbuf, L.sink);
 }
 
@@ -315,13 +318,19 @@ int main(int argc, char **argv) {
     fn_ref(L);
     CHK(hipDeviceSynchronize());
     CHK(hipMemcpy(L.Tref, L.T, L.n * 8, hipMemcpyDeviceToDevice));
-    run(L, fn_ref, "w<64,2,2,8> (product)", reps);
+    run(L, fn_ref, "w<64,2,2,8> (product, tail)", reps);
+    g_tail = false;
+    run(L, fn_ref, "w<64,2,2,8> (no tail)", reps);
+    run(L, fn_d<8, 2, 512, 1>, "d<8 waves, DT 2, 512 rows> no tail", reps);
+    g_tail = true;
     run(L, fn_d<8, 2, 512, 1>, "d<8 waves, DT 2, 512 rows>", reps);
     run(L, fn_d<8, 1, 512, 1>, "d<8 waves, DT 1, 512 rows>", reps);
     run(L, fn_d<4, 2, 512, 2>, "d<4 waves x2, DT 2, 512 rows>", reps);
     run(L, fn_d<4, 3, 512, 1>, "d<4 waves x1, DT 3, 512 rows>", reps);
     run(L, fn_d<8, 2, 1024, 1>, "d<8 waves, DT 2, 1024 rows>", reps);
     run(L, fn_d<4, 2, 1024, 2>, "d<4 waves x2, DT 2, 1024 rows>", reps);
-    run(L, fn_ref, "w<64,2,2,8> (product)", reps);
+    run(L, fn_ref, "w<64,2,2,8> (product, tail)", reps);
+    g_tail = false;
+    run(L, fn_ref, "w<64,2,2,8> (no tail)", reps);
     return 0;
 }

@@ -988,7 +988,7 @@ typedef void (*LaunchFn)(Lab &L);
 // the engine's k_flushw<64> twice: slots 0..63, then 64..127 (same chain)
 static void fn_ref(Lab &L) {
     const int64_t ntiles = (L.g.ncols + 127) / 128;
-    const int64_t rows = 512, nitems = ntiles * ((L.g.nloc + rows - 1) / rows);
+    const int64_t rows = 512, nitems = flush_nitems(ntiles, rows, L.g.nloc);
     for (int h = 0; h < L.K / 64; h++) {
         L.reset_state(64);
         hipLaunchKernelGGL((k_flushw<64, 2, 2, 4>), dim3(512), dim3(256), 0, 0, L.g.T, L.g, L.st,
@@ -1000,7 +1000,7 @@ static void fn_ref(Lab &L) {
 template <int KMAX, int NB, int LB, int R>
 static void fn_w(Lab &L) {
     const int64_t ntiles = (L.g.ncols + 127) / 128;
-    const int64_t nitems = ntiles * ((L.g.nloc + R - 1) / R);
+    const int64_t nitems = flush_nitems(ntiles, R, L.g.nloc);
     L.reset_state(L.K);
     hipLaunchKernelGGL((k_flushw<KMAX, NB, LB, 4>), dim3((unsigned)std::min<int64_t>(nitems, 256 * LB)), dim3(256), 0,
                        0, L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, (int64_t)R, 1);
@@ -1089,7 +1089,7 @@ static void fn_g(Lab &L) {
 // 96-slot reference: the product's k_flushw<96> (bitwise = the fma chain, tests/test_gpu_defer.py)
 static void fn_ref96(Lab &L) {
     const int64_t ntiles = (L.g.ncols + 127) / 128, rows = 512;
-    const int64_t nitems = ntiles * ((L.g.nloc + rows - 1) / rows);
+    const int64_t nitems = flush_nitems(ntiles, rows, L.g.nloc);
     L.reset_state(96);
     hipLaunchKernelGGL((k_flushw<96, 2, 2, 4>), dim3((unsigned)std::min<int64_t>(nitems, 512)), dim3(256), 0, 0, L.g.T,
                        L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, rows, 1);

@@ -239,7 +239,7 @@ static void fn_ref(Lab &L) {   // the product's launch (launch_flush_main, 64 sl
     h.npend = 64;
     CHK(hipMemcpyAsync(L.st, &h, sizeof h, hipMemcpyHostToDevice, 0));
     const int64_t ntiles = (L.g.ncols + 255) / 256, rows = 512;
-    const int64_t nitems = ntiles * ((L.g.nloc + rows - 1) / rows);
+    const int64_t nitems = flush_nitems(ntiles, rows, L.g.nloc);
     const int64_t nblocks = std::min<int64_t>(nitems, 512);
     hipLaunchKernelGGL((k_flushw<64, 2, 2, 8>), dim3((unsigned)((nblocks + 1) / 2)), dim3(512), 0, 0, L.g.T, L.g, L.st,
                        L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, rows, 1);
