@@ -47,8 +47,8 @@ __device__ __forceinline__ void vm_wait() {
 // go to a sink), so the counted vmcnt waits are exact. All LDS is one dynamic
 // array (a second __shared__ object makes hipcc wait vmcnt(0) before LDS
 // reads, cdna_hip_programming.md "Projection GEMM" item 4(a)).
-template <int KMAX, int WPB, int DT>
-__global__ __launch_bounds__(64 * WPB, 1) void k_flushd(double *__restrict__ T, Geo g, DevState *__restrict__ st,
+template <int KMAX, int WPB, int DT, int MINB = 1>
+__global__ __launch_bounds__(64 * WPB, MINB) void k_flushd(double *__restrict__ T, Geo g, DevState *__restrict__ st,
                                                         const double *__restrict__ Pbuf,
                                                         const double *__restrict__ Cbuf, int64_t cs, int64_t ntiles,
                                                         int64_t nitems, int64_t rows, int skip,
@@ -228,22 +228,32 @@ static void fn_ref(Lab &L) {
                        L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, rows, 1);
 }
 
-template <int WPB, int DT, int R, int BPC>
+template <int WPB, int DT, int R, int BPC, int KM = 64, int MINB = 1>
 static void fn_d(Lab &L) {
     const int64_t tw = 32 * WPB, ntiles = (L.g.ncols + tw - 1) / tw;
     const int64_t rows = g_tail ? R : -R;
     const int64_t nitems = flush_nitems(ntiles, rows, L.g.nloc);
-    const size_t lds = flushd_lds<64, WPB, DT>();
+    const size_t lds = flushd_lds<KM, WPB, DT>();
     static bool set = false;
     if (!set) {
-        CHK(hipFuncSetAttribute((const void *)k_flushd<64, WPB, DT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        CHK(hipFuncSetAttribute((const void *)k_flushd<KM, WPB, DT, MINB>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
         set = true;
     }
-    L.reset_state(64);
-    hipLaunchKernelGGL((k_flushd<64, WPB, DT>), dim3((unsigned)std::min<int64_t>(nitems, 256 * BPC)), dim3(64 * WPB),
+    L.reset_state(KM);
+    hipLaunchKernelGGL((k_flushd<KM, WPB, DT, MINB>), dim3((unsigned)std::min<int64_t>(nitems, 256 * BPC)), dim3(64 * WPB),
                        lds, 0, L.g.T, L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, rows, 1,
                        (const double *)L.zbuf, L.sink);
+}
+
+// the product's launch of k_flushw<96> (launch_flush_main: 4-wave blocks, 128-column tiles, 2 per CU)
+template <int R = 512>
+static void fn_ref96(Lab &L) {
+    const int64_t ntiles = (L.g.ncols + 127) / 128, rows = g_tail ? R : -R;
+    const int64_t nitems = flush_nitems(ntiles, rows, L.g.nloc);
+    L.reset_state(96);
+    hipLaunchKernelGGL((k_flushw<96, 2, 2, 4>), dim3((unsigned)std::min<int64_t>(nitems, 512)), dim3(256), 0, 0, L.g.T,
+                       L.g, L.st, L.Pbuf, L.Cbuf, L.cs, ntiles, nitems, rows, 1);
 }
 
 static double run(Lab &L, LaunchFn fn, const char *name, int reps) {
@@ -287,7 +297,9 @@ int main(int argc, char **argv) {
     const int64_t ncols = nstruct + m + 1, ld = (ncols + 63) / 64 * 64;
     L.n = m * ld;
     L.cs = (m + 63) / 64 * 64;
-    const int SL = 64;
+    const int K = getenv("LAB_K") ? atoi(getenv("LAB_K")) : 64;   // 64 (config 3's block) or 96 (config 4's)
+    const int SL = K;
+    L.K = K;
     CHK(hipMalloc(&L.T, L.n * 8));
     CHK(hipMalloc(&L.T0, L.n * 8));
     CHK(hipMalloc(&L.Tref, L.n * 8));
@@ -312,9 +324,26 @@ int main(int argc, char **argv) {
     L.g.m = m;
     CHK(hipEventCreate(&L.e0));
     CHK(hipEventCreate(&L.e1));
-    printf("flush64 lab: %lld rows x %lld cols (ld %lld), K=64, P zero for columns > %lld\n", (long long)m,
-           (long long)ncols, (long long)ld, (long long)nstruct);
+    printf("flush64 lab: %lld rows x %lld cols (ld %lld), K=%d, P zero for columns > %lld\n", (long long)m,
+           (long long)ncols, (long long)ld, K, (long long)nstruct);
     CHK(hipMemcpy(L.T, L.T0, L.n * 8, hipMemcpyDeviceToDevice));
+    if (K == 96) {
+        fn_ref96<512>(L);
+        CHK(hipDeviceSynchronize());
+        CHK(hipMemcpy(L.Tref, L.T, L.n * 8, hipMemcpyDeviceToDevice));
+        for (int rep = 0; rep < 2; rep++) {
+            run(L, fn_ref96<512>, "w<96,2,2,4> (product, 512 rows)", reps);
+            run(L, fn_ref96<1024>, "w<96,2,2,4> 1024 rows", reps);
+            run(L, fn_ref96<2048>, "w<96,2,2,4> 2048 rows", reps);
+            run(L, fn_d<12, 1, 512, 1, 96>, "d<96: 12 waves x1, DT 1, 512 rows>", reps);
+            run(L, fn_d<12, 1, 1024, 1, 96>, "d<96: 12 waves x1, DT 1, 1024 rows>", reps);
+            run(L, fn_d<12, 1, 2048, 1, 96>, "d<96: 12 waves x1, DT 1, 2048 rows>", reps);
+            run(L, fn_d<4, 1, 512, 2, 96>, "d<96: 4 waves x2, DT 1, 512 rows>", reps);
+            run(L, fn_d<4, 1, 1024, 2, 96>, "d<96: 4 waves x2, DT 1, 1024 rows>", reps);
+            run(L, fn_d<4, 1, 2048, 2, 96>, "d<96: 4 waves x2, DT 1, 2048 rows>", reps);
+        }
+        return 0;
+    }
     fn_ref(L);
     CHK(hipDeviceSynchronize());
     CHK(hipMemcpy(L.Tref, L.T, L.n * 8, hipMemcpyDeviceToDevice));
@@ -327,6 +356,7 @@ int main(int argc, char **argv) {
     run(L, fn_d<8, 1, 512, 1>, "d<8 waves, DT 1, 512 rows>", reps);
     run(L, fn_d<4, 2, 512, 2>, "d<4 waves x2, DT 2, 512 rows>", reps);
     run(L, fn_d<4, 3, 512, 1>, "d<4 waves x1, DT 3, 512 rows>", reps);
+    run(L, fn_d<4, 1, 512, 3, 64, 3>, "d<4 waves x3, DT 1, 512 rows>", reps);
     run(L, fn_d<8, 2, 1024, 1>, "d<8 waves, DT 2, 1024 rows>", reps);
     run(L, fn_d<4, 2, 1024, 2>, "d<4 waves x2, DT 2, 1024 rows>", reps);
     run(L, fn_ref, "w<64,2,2,8> (product, tail)", reps);
