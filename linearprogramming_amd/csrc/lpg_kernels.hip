@@ -2391,6 +2391,17 @@ static bool flush_tail_on() {
     return on != 0;
 }
 
+// item height of the banded pass (LPG_FLUSH_ROWS overrides the default, a
+// multiple of 64 from 64 to 8192; A/B runs)
+static int64_t flush_rows_env(int64_t def) {
+    static const int64_t v = [] {
+        const char *e = getenv("LPG_FLUSH_ROWS");
+        const long r = e ? atol(e) : 0;
+        return (int64_t)((r >= 64 && r <= 8192 && r % 64 == 0) ? r : 0);
+    }();
+    return v ? v : def;
+}
+
 // which: -1 = default (k_flushw), 0 = k_flushm (blocks of <= 32 pivots),
 // 1 = k_flushw (LPG_FLUSH_KERNEL=m|w, tests). Both bitwise.
 int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which) {
@@ -2402,7 +2413,7 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
     hipStream_t stream = (hipStream_t)L.stream;
     if (kmax >= 64) which = 1;                              // k_flushm's C tile caps it at 32 slots
     if (which == 1) {
-        // k_flushw: 4-wave blocks, 128-column x 512-row items swept in 16-row
+        // k_flushw: 4-wave blocks, 128-column x 2048-row items swept in 16-row
         // bands with a 2-deep LDS ring of multipliers; small tableaus shrink
         // the items until they fill the chip
         // 64 slots: 8-wave blocks over 256-column tiles (one B fragment load
@@ -2411,9 +2422,13 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
         constexpr int kW64 = 8;
         const int tw = kmax == 64 ? 32 * kW64 : 128;   // tile width: 32 columns per wave
         const int64_t ntiles = (g.ncols + tw - 1) / tw;
-        // (taller items measured at config 4: 1024 / 2048 rows within 1% of 512;
-        // 128 rows 13% slower)
-        int64_t rows = 512;
+        // Items of up to 2048 rows (round 4, with the short tail items): config 4
+        // pass 34.5 -> 33.5 ms per 96-pivot block at 2048 vs 512 rows, 4096 /
+        // 8192 within 0.6% of 2048; config 3 (halved to 1024 by the fill rule
+        // below) 1.69 -> 1.64 ms (profiles/r04_c4_rows*.log, r04_c3_rows*.log).
+        // Round 3, before the tail items: 1024 / 2048 within 1% of 512, 128
+        // rows 13% slower.
+        int64_t rows = flush_rows_env(2048);
         while (rows > 64 && ntiles * ((g.nloc + rows - 1) / rows) < 2048) rows /= 2;
         if (!flush_tail_on()) rows = -rows;
         const int64_t nitems = flush_nitems(ntiles, rows, g.nloc);
