@@ -683,13 +683,18 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
         dR = *(const d2 *)(T + rR * g.ld + 2 * j2);
     }
     const double cM = -Cs[rM], cR = -Cs[rR];
-    // kPF = 128: two banks of 64 slots (blocks of up to 128 pivots); bank 1
-    // holds slots 64 .. 127 in lanes 0 .. 63 and its P rows are loaded after
-    // bank 0's chain (the registers of a 128-row prefetch are not there: one
-    // more memory round trip, ~1 us, on pivots 65 .. 128 of a block)
-    constexpr int B0 = kPF < 64 ? kPF : 64;
-    constexpr bool TWO = kPF > 64;
-    static_assert(kPF <= 64 || kPF == 128, "prefetch slots");
+    // kPF = 96 / 128: two banks of B0 = 48 / 64 slots (blocks of up to 96 /
+    // 128 pivots); bank 1 holds slots B0 .. kPF - 1 in lanes 0 .. B1 - 1 and
+    // its P rows are loaded after bank 0's chain (the registers of a whole
+    // prefetch are not there: one more memory round trip, ~1 us). kPF = 96
+    // exists for the grid: 48-slot banks keep the kernel at 2 waves per SIMD,
+    // so config 4's 385 blocks run in one round on 256 CUs where kPF = 64's
+    // one wave per SIMD needed two (~8-10 us per pivot, profiles/r04_phase_probe_c4.log)
+    constexpr int B0 = kPF < 64 ? kPF : (kPF == 96 ? 48 : 64);
+    constexpr int B1 = kPF > 64 ? kPF - B0 : 0;
+    constexpr bool TWO = B1 > 0;
+    static_assert(kPF <= 64 || kPF == 96 || kPF == 128, "prefetch slots");
+    static_assert(B1 <= B0 && B1 <= 64, "bank 1 reuses bank 0's registers, one slot per lane");
     const int npf = D.q < B0 ? D.q : B0;
     // slots past the block are (+0, +0) and their multiplier is -0: the chain
     // step fma(-0, +0, x) == x for every x, so the loop below needs no bound
@@ -700,8 +705,8 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
 #pragma unroll
     for (int u = 0; u < B0; u++)
         pq[u] = *(const d2 *)((u < npf ? D.Pbuf + (int64_t)u * g.ld : D.zrow) + jc);
-    const int64_t rqv = lane < D.q ? D.rq[lane] : -1;   // lane q of every wave holds r_q
-    const int64_t rqv1 = TWO && 64 + lane < D.q ? D.rq[64 + lane] : -1;   // bank 1: r_{64 + lane}
+    const int64_t rqv = lane < B0 && lane < D.q ? D.rq[lane] : -1;   // lane q of every wave holds r_q
+    const int64_t rqv1 = TWO && lane < B1 && B0 + lane < D.q ? D.rq[B0 + lane] : -1;   // bank 1: r_{B0 + lane}
     const int2 lj = col ? ((const int2 *)D.colmap)[j2] : int2{0, 0};   // logical indices of the two columns
     // MODE 1: the allreduce of P runs whether or not a pivot does (the loop
     // may have ended): then every rank sends the identity, -0
@@ -756,16 +761,16 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
     // the multiplier read back from lane q (v_readlane: no LDS, no barrier)
     d2 t = d2{0.0, 0.0};
     if (col && own) t = *(const d2 *)(T + rl * g.ld + 2 * j2);
-    const double cl = (own && lane < D.q) ? -D.Cbuf[(int64_t)lane * D.cs + rl] : -0.0;
-    const double cl1 = (TWO && own && 64 + lane < D.q) ? -D.Cbuf[(int64_t)(64 + lane) * D.cs + rl] : -0.0;
-    const unsigned long long hit = __ballot(own && lane < D.q && rqv == rl);
-    const unsigned long long hit1 = TWO ? __ballot(own && 64 + lane < D.q && rqv1 == rl) : 0ull;
-    const int qs = hit1 ? 127 - __clzll((long long)hit1) : hit ? 63 - __clzll((long long)hit) : -1;
+    const double cl = (own && lane < B0 && lane < D.q) ? -D.Cbuf[(int64_t)lane * D.cs + rl] : -0.0;
+    const double cl1 = (TWO && own && lane < B1 && B0 + lane < D.q) ? -D.Cbuf[(int64_t)(B0 + lane) * D.cs + rl] : -0.0;
+    const unsigned long long hit = __ballot(own && lane < B0 && lane < D.q && rqv == rl);
+    const unsigned long long hit1 = TWO ? __ballot(own && lane < B1 && B0 + lane < D.q && rqv1 == rl) : 0ull;
+    const int qs = hit1 ? B0 + 63 - __clzll((long long)hit1) : hit ? 63 - __clzll((long long)hit) : -1;
     LPG_PH(0, 3);
     PricePart pbest{0.0, -1, 0, 0};
     const uint64_t clb = (uint64_t)__double_as_longlong(cl);
     const uint64_t clb1 = (uint64_t)__double_as_longlong(cl1);
-    const int npf1 = TWO && D.q > 64 ? D.q - 64 : 0;
+    const int npf1 = TWO && D.q > B0 ? D.q - B0 : 0;
     // The chain runs in every lane (EXEC full, uniform branches only): a
     // readlane returns the source lane's register whether or not that lane
     // was active when the register was written, so the multipliers must never
@@ -788,22 +793,22 @@ __global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, De
             t.y = u == qs ? pq[u].y : (u > qs ? fy : t.y);
         }
     }
-    if (TWO && D.q > 64) {                  // bank 1: slots 64 .. D.q - 1 (uniform)
+    if (TWO && D.q > B0) {                  // bank 1: slots B0 .. D.q - 1 (uniform)
         asm volatile("" ::: "memory");      // its loads stay behind bank 0's chain
 #pragma unroll
-        for (int u = 0; u < 64; u++)
-            pq[u] = *(const d2 *)((u < npf1 ? D.Pbuf + (int64_t)(64 + u) * g.ld : D.zrow) + jc);
-        const int qs1 = qs - 64;
+        for (int u = 0; u < B1; u++)
+            pq[u] = *(const d2 *)((u < npf1 ? D.Pbuf + (int64_t)(B0 + u) * g.ld : D.zrow) + jc);
+        const int qs1 = qs - B0;
         if (qs1 < 0) {
 #pragma unroll
-            for (int u = 0; u < 64; u++) {
+            for (int u = 0; u < B1; u++) {
                 const double c = __longlong_as_double((long long)rdl64(clb1, u));
                 t.x = fma(c, pq[u].x, t.x);
                 t.y = fma(c, pq[u].y, t.y);
             }
         } else {
 #pragma unroll
-            for (int u = 0; u < 64; u++) {
+            for (int u = 0; u < B1; u++) {
                 const double c = __longlong_as_double((long long)rdl64(clb1, u));
                 const double fx = fma(c, pq[u].x, t.x), fy = fma(c, pq[u].y, t.y);
                 t.x = u == qs1 ? pq[u].x : (u > qs1 ? fx : t.x);
@@ -1050,6 +1055,17 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
         b = ob;
         a = oa;
     }
+    // objective rows past the grid: the single-rank launch covers only the
+    // constraint rows (pivot_d_blocks(g, 2, nt): config 4's 65536 rows take
+    // 256 blocks, one per CU, where 257 left one block for a second round at
+    // one wave per SIMD); block 0 then writes their C_{t+1} entries, which
+    // are column k as stored (the objective rows are current), and the
+    // candidates of the blocks the grid left out, none (the consumers read
+    // pivot_d_blocks(g, 1, nt) of them). Loaded after the chain (no
+    // registers held across it), stored after the block argmin.
+    const int64_t iob = g.nloc + threadIdx.x;
+    const bool fold = blockIdx.x == 0 && threadIdx.x < g.nobj && iob >= (int64_t)gridDim.x * NT;
+    const double foa = fold ? T[iob * g.ld + kp] : 0.0;
     if (row) {
         Cs1[i] = a;
         if (crow && a > g.eps_piv) {
@@ -1065,6 +1081,15 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
     LPG_PH(1, 4);
     best = block_argmin_cand<NT / 64>(best);
     if (threadIdx.x == 0) part[blockIdx.x] = best;
+    if (blockIdx.x == 0) {
+        if (fold) Cs1[iob] = foa;
+        const int64_t bn = (int64_t)gridDim.x + threadIdx.x;   // the grid leaves out at most NT blocks
+        if (bn * NT < nrows) {                                 // {0, 0, 0, row -1}: none
+            double2 *w = (double2 *)(part + bn);
+            w[0] = double2{0.0, 0.0};
+            w[1] = double2{0.0, __longlong_as_double(-1ll)};
+        }
+    }
     if (PUSH && threadIdx.x == 0) {
         const uint32_t tg = X.tag + 1;
         const uint64_t th = (uint64_t)__double_as_longlong(best.theta), pv = (uint64_t)__double_as_longlong(best.piv);
@@ -1094,11 +1119,19 @@ int debug_phases(unsigned long long *out, int reset) {
 
 // prefetch slots of k_prep_d / k_select_d: the pending chain rounded up to
 // 16 (padding slots cost a load and two fmas each, ~1.4 us per kernel for 32
-// of them), two banks of 64 past 64 pending pivots
+// of them), two banks of 64 past 64 pending pivots; k_prep_d takes two banks
+// of 48 from 48 to 95 pending pivots (2 waves per SIMD, see kPF = 96)
 static int pivot_pf(int q) { return q < 16 ? 16 : q < 32 ? 32 : q < 48 ? 48 : q < 64 ? 64 : 128; }
+static int prep_pf(int q) { return q < 48 ? pivot_pf(q) : q < 96 ? 96 : 128; }
 
+// which 0: k_prep_d's column blocks; 1: k_select_d's row blocks covering the
+// objective rows (its candidate count, every form); 2: the single-rank pair's
+// select grid, the constraint rows only (k_select_d folds the objective rows
+// and the missing blocks' candidates into block 0)
 int pivot_d_blocks(const Geo &g, int which, int nt) {
-    return which == 0 ? (int)(((g.ncols + 1) / 2 + nt - 1) / nt) : (int)((g.nloc + g.nobj + nt - 1) / nt);
+    if (which == 0) return (int)(((g.ncols + 1) / 2 + nt - 1) / nt);
+    if (which == 2) return (int)std::max<int64_t>(1, (g.nloc + nt - 1) / nt);
+    return (int)((g.nloc + g.nobj + nt - 1) / nt);
 }
 
 int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s, int s1, Cand *part, int nsel,
@@ -1109,34 +1142,29 @@ int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s,
     // oracle at m = 16384 (first pivots identical, later ones not), so they
     // are not offered.
     if (nt != 256 || npp != pivot_d_blocks(g, 0, nt) || nsel != pivot_d_blocks(g, 1, nt)) return -1;
+    const int nselg = pivot_d_blocks(g, 2, nt);   // the grid: constraint rows only (k_select_d folds the rest)
     hipStream_t stream = (hipStream_t)L.stream;
     const Xch X0{};
-#define LPG_PD(R, PF, NT)                                                                                             \
-    do {                                                                                                              \
-        hipLaunchKernelGGL((k_prep_d<R, PF, NT, 0>), dim3(npp), dim3(NT), 0, stream, g.T, g, st, s, part, nsel, P,     \
-                           Cs, pp, D, X0);                                                                            \
-        hipLaunchKernelGGL((k_select_d<R, PF, NT, false>), dim3(nsel), dim3(NT), 0, stream, g.T, g, st, s, s1, Cs, Cs1, \
-                           pp, npp, basis, part, D, X0);                                                              \
+#define LPG_PD(R, PFP, PFS)                                                                                            \
+    do {                                                                                                               \
+        hipLaunchKernelGGL((k_prep_d<R, PFP, 256, 0>), dim3(npp), dim3(256), 0, stream, g.T, g, st, s, part, nsel, P,   \
+                           Cs, pp, D, X0);                                                                             \
+        hipLaunchKernelGGL((k_select_d<R, PFS, 256, false>), dim3(nselg), dim3(256), 0, stream, g.T, g, st, s, s1, Cs,  \
+                           Cs1, pp, npp, basis, part, D, X0);                                                          \
     } while (0)
-#define LPG_PD_NT(R, PF)                   \
-    do {                                   \
-        LPG_PD(R, PF, 256);                \
+#define LPG_PD_R(R)                                          \
+    do {                                                     \
+        const int pf = pivot_pf(D.q), pp_ = prep_pf(D.q);    \
+        if (pf == 16) LPG_PD(R, 16, 16);                     \
+        else if (pf == 32) LPG_PD(R, 32, 32);                \
+        else if (pf == 48) LPG_PD(R, 48, 48);                \
+        else if (pf == 64) LPG_PD(R, 96, 64);                \
+        else if (pp_ == 96) LPG_PD(R, 96, 128);              \
+        else LPG_PD(R, 128, 128);                            \
     } while (0)
-    const int pf = pivot_pf(D.q);
-    if (rule == RULE_BLAND) {
-        if (pf == 16) LPG_PD_NT(RULE_BLAND, 16);
-        else if (pf == 32) LPG_PD_NT(RULE_BLAND, 32);
-        else if (pf == 48) LPG_PD_NT(RULE_BLAND, 48);
-        else if (pf == 64) LPG_PD_NT(RULE_BLAND, 64);
-        else LPG_PD_NT(RULE_BLAND, 128);
-    } else {
-        if (pf == 16) LPG_PD_NT(RULE_DANTZIG, 16);
-        else if (pf == 32) LPG_PD_NT(RULE_DANTZIG, 32);
-        else if (pf == 48) LPG_PD_NT(RULE_DANTZIG, 48);
-        else if (pf == 64) LPG_PD_NT(RULE_DANTZIG, 64);
-        else LPG_PD_NT(RULE_DANTZIG, 128);
-    }
-#undef LPG_PD_NT
+    if (rule == RULE_BLAND) LPG_PD_R(RULE_BLAND);
+    else LPG_PD_R(RULE_DANTZIG);
+#undef LPG_PD_R
 #undef LPG_PD
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -1151,18 +1179,18 @@ int launch_prep_dm(const Launch &L, const Geo &g, int rule, DevState *st, int s,
 #define LPG_PM(R, PF)                                                                                                 \
     hipLaunchKernelGGL((k_prep_d<R, PF, 256, 1>), dim3(npp_d), dim3(256), 0, stream, g.T, g, st, s, cand, ncand, P,    \
                        Cs, nullptr, D, X0)
-    const int pf = pivot_pf(D.q);   // as launch_pivot_d
+    const int pf = prep_pf(D.q);   // as launch_pivot_d
     if (rule == RULE_BLAND) {
         if (pf == 16) LPG_PM(RULE_BLAND, 16);
         else if (pf == 32) LPG_PM(RULE_BLAND, 32);
         else if (pf == 48) LPG_PM(RULE_BLAND, 48);
-        else if (pf == 64) LPG_PM(RULE_BLAND, 64);
+        else if (pf == 96) LPG_PM(RULE_BLAND, 96);
         else LPG_PM(RULE_BLAND, 128);
     } else {
         if (pf == 16) LPG_PM(RULE_DANTZIG, 16);
         else if (pf == 32) LPG_PM(RULE_DANTZIG, 32);
         else if (pf == 48) LPG_PM(RULE_DANTZIG, 48);
-        else if (pf == 64) LPG_PM(RULE_DANTZIG, 64);
+        else if (pf == 96) LPG_PM(RULE_DANTZIG, 96);
         else LPG_PM(RULE_DANTZIG, 128);
     }
 #undef LPG_PM
@@ -1216,18 +1244,18 @@ int launch_prep_x(const Launch &L, const Geo &g, int rule, DevState *st, int s, 
 #define LPG_PX(R, PF)                                                                                                 \
     hipLaunchKernelGGL((k_prep_d<R, PF, 256, 2>), dim3(npp_d), dim3(256), 0, stream, g.T, g, st, s, cand, ncand, P,    \
                        Cs, pp, D, X)
-    const int pf = pivot_pf(D.q);   // as launch_pivot_d
+    const int pf = prep_pf(D.q);   // as launch_pivot_d
     if (rule == RULE_BLAND) {
         if (pf == 16) LPG_PX(RULE_BLAND, 16);
         else if (pf == 32) LPG_PX(RULE_BLAND, 32);
         else if (pf == 48) LPG_PX(RULE_BLAND, 48);
-        else if (pf == 64) LPG_PX(RULE_BLAND, 64);
+        else if (pf == 96) LPG_PX(RULE_BLAND, 96);
         else LPG_PX(RULE_BLAND, 128);
     } else {
         if (pf == 16) LPG_PX(RULE_DANTZIG, 16);
         else if (pf == 32) LPG_PX(RULE_DANTZIG, 32);
         else if (pf == 48) LPG_PX(RULE_DANTZIG, 48);
-        else if (pf == 64) LPG_PX(RULE_DANTZIG, 64);
+        else if (pf == 96) LPG_PX(RULE_DANTZIG, 96);
         else LPG_PX(RULE_DANTZIG, 128);
     }
 #undef LPG_PX

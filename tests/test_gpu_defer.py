@@ -232,3 +232,35 @@ def test_wide_tableau_more_partials_than_threads(lpg, monkeypatch, k, rule, cap)
     assert res.status == (1 if rule == 0 else 4)
     assert res.objective == ores.objective
     _assert_same(e, o, m)
+
+
+@pytest.mark.parametrize("k", [64, 96, 128])
+@pytest.mark.parametrize("m,n,seed,kind,rule,big_m", [(512, 700, 5, 0, 0, False), (768, 500, 6, 1, 1, False),
+                                                      (767, 600, 9, 2, 0, True)])
+def test_pair_select_grid_folds_objective_rows(lpg, monkeypatch, k, m, n, seed, kind, rule, big_m):
+    """The single-rank pair (LPG_PERSIST=0) launches k_select_d over the
+    constraint rows only; block 0 writes the objective rows' C entries and a
+    'none' candidate for each block the grid left out (m = 512, 768: every
+    objective row folded; m = 767 with the big-M row: the second one only).
+    Blocks of 64 / 96 / 128 also run k_prep_d's two-bank forms (48 + 48 slots
+    from 48 pending pivots, 64 + 64 from 96). Bitwise the oracle throughout."""
+    monkeypatch.setenv("LPG_PERSIST", "0")
+    flags = lpg._lib.FLAG_BIG_M if big_m else 0
+    monkeypatch.setenv("LPG_DEFER", str(k))
+    e = lpg.Engine(m, n + m + 1, flags=flags)
+    monkeypatch.delenv("LPG_DEFER")
+    o = Oracle(m, n + m + 1, nobj=2 if big_m else 1)
+    e.generate(n, seed, kind)
+    o.generate(n, seed, kind)
+    cap = 3000
+    if big_m:
+        art_first = 1 + n + (m + 1) // 2
+        res, ores = e.solve_big_m(art_first, None, cap, rule), o.solve_big_m(art_first, None, cap, rule)
+    else:
+        res, ores = e.solve(cap, rule), o.solve(cap, rule)
+    assert res.status == ores.status and res.pivots == ores.pivots > 48
+    assert res.objective == ores.objective
+    rows = m + (2 if big_m else 1)
+    assert _log(e) == _log(o)
+    assert np.array_equal(e.get_basis(), o.get_basis())
+    assert np.array_equal(e.get_rows(0, rows), o.get_rows())

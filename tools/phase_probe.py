@@ -32,7 +32,7 @@ for q in range(K):
     e.enqueue(1, 0)
     torch.cuda.synchronize()
     lib.lpg_debug_phases(buf, 0)
-    if q in (0, 1, 16, K // 2 - 1, K // 2, 3 * K // 4, K - 1):
+    if q in (0, 1, 16, K // 2 - 1, K // 2, 63, 64, 3 * K // 4, K - 1):
         for kern in (0, 1):
             ph = [buf[kern * 16 + j] for j in range(16)]
             t0 = ph[14]
