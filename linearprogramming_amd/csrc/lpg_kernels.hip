@@ -2430,6 +2430,16 @@ static int64_t flush_rows_env(int64_t def) {
     return v ? v : def;
 }
 
+// the fill rule's item count (LPG_FLUSH_MINITEMS overrides, 256 .. 65536; A/B runs)
+static int64_t flush_minitems_env(int64_t def) {
+    static const int64_t v = [] {
+        const char *e = getenv("LPG_FLUSH_MINITEMS");
+        const long r = e ? atol(e) : 0;
+        return (int64_t)((r >= 256 && r <= 65536) ? r : 0);
+    }();
+    return v ? v : def;
+}
+
 // which: -1 = default (k_flushw), 0 = k_flushm (blocks of <= 32 pivots),
 // 1 = k_flushw (LPG_FLUSH_KERNEL=m|w, tests). Both bitwise.
 int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which) {
@@ -2457,7 +2467,8 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
         // Round 3, before the tail items: 1024 / 2048 within 1% of 512, 128
         // rows 13% slower.
         int64_t rows = flush_rows_env(2048);
-        while (rows > 64 && ntiles * ((g.nloc + rows - 1) / rows) < 2048) rows /= 2;
+        const int64_t minitems = flush_minitems_env(2048);
+        while (rows > 64 && ntiles * ((g.nloc + rows - 1) / rows) < minitems) rows /= 2;
         if (!flush_tail_on()) rows = -rows;
         const int64_t nitems = flush_nitems(ntiles, rows, g.nloc);
         const int lb = kmax == 128 ? 1 : kmax == 96 ? 2 : kmax == 64 ? 2 : 3;   // VGPRs: 184 at 64 slots, <= 128 below
