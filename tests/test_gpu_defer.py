@@ -264,3 +264,19 @@ def test_pair_select_grid_folds_objective_rows(lpg, monkeypatch, k, m, n, seed, 
     assert _log(e) == _log(o)
     assert np.array_equal(e.get_basis(), o.get_basis())
     assert np.array_equal(e.get_rows(0, rows), o.get_rows())
+
+
+
+def test_96_slot_pass_many_items(lpg, monkeypatch):
+    """The 96-slot block pass over many items and the short tail items
+    (4096 x 12289, 2048-row items halved to fill the chip), bitwise the oracle
+    after 3 whole blocks and a partial one."""
+    m, n = 4096, 8192
+    e = _engine(lpg, monkeypatch, 96, m, n + m + 1)
+    o = Oracle(m, n + m + 1, nthreads=8)
+    e.generate(n, 20220518, 0)
+    o.generate(n, 20220518, 0)
+    res = e.solve(3 * 96 + 17, 0)
+    ores = o.solve(3 * 96 + 17, 0)
+    assert res.status == ores.status and res.pivots == ores.pivots == 3 * 96 + 17
+    _assert_same(e, o, m)
