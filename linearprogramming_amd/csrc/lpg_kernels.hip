@@ -921,10 +921,13 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
         ob = T[i * g.ld];
         csi = Cs[i];
     }
-    // kPF = 128: two banks of 64 slots (blocks of up to 128 pivots; k_prep_d)
-    constexpr int B0 = kPF < 64 ? kPF : 64;
-    constexpr bool TWO = kPF > 64;
-    static_assert(kPF <= 64 || kPF == 128, "prefetch slots");
+    // kPF = 96 / 128: two banks of B0 = 48 / 64 slots (blocks of up to 96 /
+    // 128 pivots; k_prep_d): 96 chain steps instead of 128 from 64 to 95
+    // pending pivots
+    constexpr int B0 = kPF < 64 ? kPF : (kPF == 96 ? 48 : 64);
+    constexpr int B1 = kPF > 64 ? kPF - B0 : 0;
+    constexpr bool TWO = B1 > 0;
+    static_assert(kPF <= 64 || kPF == 96 || kPF == 128, "prefetch slots");
     const int npf = D.q < B0 ? D.q : B0;
     // slots past the pending block: +0 (with P entries +0 below: no-op steps).
     // The loads are unconditional (a clamped address, then a select): a load
@@ -937,24 +940,24 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
         const double v = D.Cbuf[(int64_t)(u < npf ? u : 0) * D.cs + ic];
         cv[u] = (u < npf && crow) ? v : 0.0;
     }
-    double cv1[TWO ? 64 : 1];        // bank 1: slots 64 .. D.q - 1 (pivot t's own C_t is added below)
-    const int npf1 = TWO && D.q > 64 ? D.q - 64 : 0;
+    double cv1[TWO ? B1 : 1];        // bank 1: slots B0 .. D.q - 1 (pivot t's own C_t is added below)
+    const int npf1 = TWO && D.q > B0 ? D.q - B0 : 0;
 #pragma unroll
-    for (int u = 0; u < (TWO ? 64 : 1); u++) {
+    for (int u = 0; u < (TWO ? B1 : 1); u++) {
         cv1[u] = 0.0;
         if (TWO) {
-            const double v = D.Cbuf[(int64_t)(u < npf1 ? 64 + u : 0) * D.cs + ic];
+            const double v = D.Cbuf[(int64_t)(u < npf1 ? B0 + u : 0) * D.cs + ic];
             cv1[u] = (u < npf1 && crow) ? v : 0.0;
         }
     }
     // lane q of every wave holds P_q[0], r_q (q <= D.q: pivot t included);
-    // bank 1 slot 64 + q in lane q
+    // bank 1 slot B0 + q in lane q
     const bool lq = lane <= D.q;
     const double p0l = lq ? D.Pbuf[(int64_t)lane * g.ld] : 0.0;
     const int32_t rql = lq ? (int32_t)D.rq[lane] : -1;
-    const bool lq1 = TWO && 64 + lane <= D.q;
-    const double p0l1 = lq1 ? D.Pbuf[(int64_t)(64 + lane) * g.ld] : 0.0;
-    const int32_t rql1 = lq1 ? (int32_t)D.rq[64 + lane] : -1;
+    const bool lq1 = TWO && lane < B1 && B0 + lane <= D.q;
+    const double p0l1 = lq1 ? D.Pbuf[(int64_t)(B0 + lane) * g.ld] : 0.0;
+    const int32_t rql1 = lq1 ? (int32_t)D.rq[B0 + lane] : -1;
     const int64_t bkey = (RULE == RULE_BLAND && crow) ? basis[g.row0 + i] : 0;
     Slot *dst = &st->slot[s1];
     if (stt != RUNNING) {
@@ -989,7 +992,7 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
     double oa = 0.0;
     if (row) oa = T[i * g.ld + kp];
     const double pkl = lq ? D.Pbuf[(int64_t)lane * g.ld + kp] : 0.0;
-    const double pkl1 = lq1 ? D.Pbuf[(int64_t)(64 + lane) * g.ld + kp] : 0.0;
+    const double pkl1 = lq1 ? D.Pbuf[(int64_t)(B0 + lane) * g.ld + kp] : 0.0;
     LPG_PH(1, 3);
     const uint64_t p0b = (uint64_t)__double_as_longlong(p0l), pkb = (uint64_t)__double_as_longlong(pkl);
     Cand best{0.0, 0.0, 0, -1};
@@ -1026,13 +1029,13 @@ __global__ __launch_bounds__(NT) void k_select_d(const double *__restrict__ T, G
             a = hit ? qk : fa;
         }
     }
-    if (TWO && D.q >= 64) {
+    if (TWO && D.q >= B0) {
         // bank 1, pivot t included (slot D.q, multiplier -Cs): lanes past
-        // D.q - 64 read as (P = +0, r = -1) with multiplier +0
+        // D.q - B0 read as (P = +0, r = -1) with multiplier +0
         const uint64_t p0b1 = (uint64_t)__double_as_longlong(p0l1), pkb1 = (uint64_t)__double_as_longlong(pkl1);
-        const int qt = D.q - 64;
+        const int qt = D.q - B0;
 #pragma unroll
-        for (int u = 0; u < 64; u++) {
+        for (int u = 0; u < B1; u++) {
             const double q0 = __longlong_as_double((long long)rdl64(p0b1, u));
             const double qk = __longlong_as_double((long long)rdl64(pkb1, u));
             const bool hit = ii == (int32_t)rdl32((uint32_t)rql1, u);
@@ -1123,6 +1126,7 @@ int debug_phases(unsigned long long *out, int reset) {
 // of 48 from 48 to 95 pending pivots (2 waves per SIMD, see kPF = 96)
 static int pivot_pf(int q) { return q < 16 ? 16 : q < 32 ? 32 : q < 48 ? 48 : q < 64 ? 64 : 128; }
 static int prep_pf(int q) { return q < 48 ? pivot_pf(q) : q < 96 ? 96 : 128; }
+static int select_pf(int q) { return q < 64 ? pivot_pf(q) : q < 96 ? 96 : 128; }
 
 // which 0: k_prep_d's column blocks; 1: k_select_d's row blocks covering the
 // objective rows (its candidate count, every form); 2: the single-rank pair's
@@ -1154,12 +1158,12 @@ int launch_pivot_d(const Launch &L, const Geo &g, int rule, DevState *st, int s,
     } while (0)
 #define LPG_PD_R(R)                                          \
     do {                                                     \
-        const int pf = pivot_pf(D.q), pp_ = prep_pf(D.q);    \
+        const int pf = select_pf(D.q);                       \
         if (pf == 16) LPG_PD(R, 16, 16);                     \
         else if (pf == 32) LPG_PD(R, 32, 32);                \
         else if (pf == 48) LPG_PD(R, 48, 48);                \
         else if (pf == 64) LPG_PD(R, 96, 64);                \
-        else if (pp_ == 96) LPG_PD(R, 96, 128);              \
+        else if (pf == 96) LPG_PD(R, 96, 96);                \
         else LPG_PD(R, 128, 128);                            \
     } while (0)
     if (rule == RULE_BLAND) LPG_PD_R(RULE_BLAND);
@@ -1208,18 +1212,20 @@ int launch_select_dm(const Launch &L, const Geo &g, int rule, DevState *st, int 
 #define LPG_SM(R, PF)                                                                                               \
     hipLaunchKernelGGL((k_select_d<R, PF, 256, false>), dim3(nsel), dim3(256), 0, stream, g.T, g, st, s, s1, Cs, Cs1, \
                        pp, npp, basis, part, D, X0)
-    const int pf = pivot_pf(D.q);   // as launch_pivot_d
+    const int pf = select_pf(D.q);   // as launch_pivot_d
     if (rule == RULE_BLAND) {
         if (pf == 16) LPG_SM(RULE_BLAND, 16);
         else if (pf == 32) LPG_SM(RULE_BLAND, 32);
         else if (pf == 48) LPG_SM(RULE_BLAND, 48);
         else if (pf == 64) LPG_SM(RULE_BLAND, 64);
+        else if (pf == 96) LPG_SM(RULE_BLAND, 96);
         else LPG_SM(RULE_BLAND, 128);
     } else {
         if (pf == 16) LPG_SM(RULE_DANTZIG, 16);
         else if (pf == 32) LPG_SM(RULE_DANTZIG, 32);
         else if (pf == 48) LPG_SM(RULE_DANTZIG, 48);
         else if (pf == 64) LPG_SM(RULE_DANTZIG, 64);
+        else if (pf == 96) LPG_SM(RULE_DANTZIG, 96);
         else LPG_SM(RULE_DANTZIG, 128);
     }
 #undef LPG_SM
@@ -1270,18 +1276,20 @@ int launch_select_x(const Launch &L, const Geo &g, int rule, DevState *st, int s
 #define LPG_SX(R, PF)                                                                                              \
     hipLaunchKernelGGL((k_select_d<R, PF, 256, true>), dim3(nsel), dim3(256), 0, stream, g.T, g, st, s, s1, Cs, Cs1, \
                        pp, npp, basis, part, D, X)
-    const int pf = pivot_pf(D.q);
+    const int pf = select_pf(D.q);   // as launch_pivot_d
     if (rule == RULE_BLAND) {
         if (pf == 16) LPG_SX(RULE_BLAND, 16);
         else if (pf == 32) LPG_SX(RULE_BLAND, 32);
         else if (pf == 48) LPG_SX(RULE_BLAND, 48);
         else if (pf == 64) LPG_SX(RULE_BLAND, 64);
+        else if (pf == 96) LPG_SX(RULE_BLAND, 96);
         else LPG_SX(RULE_BLAND, 128);
     } else {
         if (pf == 16) LPG_SX(RULE_DANTZIG, 16);
         else if (pf == 32) LPG_SX(RULE_DANTZIG, 32);
         else if (pf == 48) LPG_SX(RULE_DANTZIG, 48);
         else if (pf == 64) LPG_SX(RULE_DANTZIG, 64);
+        else if (pf == 96) LPG_SX(RULE_DANTZIG, 96);
         else LPG_SX(RULE_DANTZIG, 128);
     }
 #undef LPG_SX
@@ -1991,7 +1999,7 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T,
 // feeds 4 chains (groups {w, 7-w, 8+w, 15-w, ...}: equal work per wave); the
 // first steps of a group, where only some of its rows have started, are
 // peeled so that every row sees exactly its own steps. K = 64: the
-// multipliers are staged in LDS too; K = 128 (128 KB of them) reads them as
+// multipliers are staged in LDS too; K = 96 / 128 (72 / 128 KB of them) read them as
 // wave-uniform loads, and r_q of slots 64 .. 127 sits in a second register.
 template <int K>
 __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict__ T, Geo g,
@@ -1999,7 +2007,8 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
                                                              const double *__restrict__ Pbuf,
                                                              const double *__restrict__ mul,
                                                              const int64_t *__restrict__ rq) {
-    static_assert((K == 64 || K == 128) && K <= LPG_DEFER_MAX && kBlock == 256, "4 waves x K/16 groups of 4 rows");
+    static_assert((K == 64 || K == 96 || K == 128) && K <= LPG_DEFER_MAX && kBlock == 256,
+                  "4 waves x K/16 groups of 4 rows");
     constexpr bool LM = K == 64;                        // multipliers in LDS
     constexpr int PW = K / (kBlock / 64);               // P rows staged per wave
     constexpr int MT = LM ? K * K / kBlock : 1;         // multipliers staged per thread
@@ -2044,10 +2053,12 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
         double x0 = sP[q0][c], x1 = sP[q0 + 1][c], x2 = sP[q0 + 2][c], x3 = sP[q0 + 3][c];
         if (!LM) {                                      // this wave's rows only: no barrier
 #pragma unroll
-            for (int k = 0; k < (LM ? 1 : K / 64); k++) {
+            for (int k = 0; k < (LM ? 1 : (K + 63) / 64); k++) {
                 const int u = c + 64 * k;
-                const d4 m = *(const d4 *)(mul + (u < np ? u : 0) * LPG_DEFER_MAX + q0);
-                *(d4 *)&sMg[LM ? 0 : w][LM ? 0 : u][0] = u < np ? m : d4{0.0, 0.0, 0.0, 0.0};
+                if (u < K) {
+                    const d4 m = *(const d4 *)(mul + (u < np ? u : 0) * LPG_DEFER_MAX + q0);
+                    *(d4 *)&sMg[LM ? 0 : w][LM ? 0 : u][0] = u < np ? m : d4{0.0, 0.0, 0.0, 0.0};
+                }
             }
         }
         auto m4 = [&](int u) {                          // mul[u][q0 .. q0 + 3]
@@ -2392,8 +2403,11 @@ int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &
     if (!kmax) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
     const int64_t ntiles_p = (g.ncols + 63) / 64;   // k_flush_pivot_rows column tiles
-    if (kmax > 64)
+    if (kmax > 96)
         hipLaunchKernelGGL(k_flush_pivot_rows<128>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
+                           D.Pbuf, D.mul, D.rq);
+    else if (kmax > 64)   // 96 slots: 60 KB of LDS, two blocks per CU (the 128-slot form's 80 KB: one)
+        hipLaunchKernelGGL(k_flush_pivot_rows<96>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
                            D.Pbuf, D.mul, D.rq);
     else
         hipLaunchKernelGGL(k_flush_pivot_rows<64>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
