@@ -657,7 +657,7 @@ __device__ bool xch_gather(const Xch &X, Cand &best) {
 // block waits for its chunk's flag and reads it; then every rank prices
 // (k_price's work, fused as in MODE 0).
 template <int RULE, int kPF, int NT, int MODE>
-__global__ __launch_bounds__(NT) void k_prep_d(double *__restrict__ T, Geo g, DevState *st, int s,
+__global__ __launch_bounds__(NT, kPF == 96 ? 2 : 1) void k_prep_d(double *__restrict__ T, Geo g, DevState *st, int s,
                                                    const Cand *__restrict__ cand, int ncand, double *__restrict__ P,
                                                    const double *__restrict__ Cs, PricePart *__restrict__ pp, Defer D,
                                                    Xch X) {
