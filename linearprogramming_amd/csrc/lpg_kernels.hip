@@ -2008,7 +2008,7 @@ __global__ __launch_bounds__(kBlock) void k_flush_pivot_rows(double *__restrict_
                                                              const double *__restrict__ mul,
                                                              const int64_t *__restrict__ rq) {
     static_assert((K == 64 || K == 96 || K == 128) && K <= LPG_DEFER_MAX && kBlock == 256,
-                  "4 waves x K/16 groups of 4 rows");
+                  "4 waves x K/16 groups of 4 rows");   // (96: measured, not launched)
     constexpr bool LM = K == 64;                        // multipliers in LDS
     constexpr int PW = K / (kBlock / 64);               // P rows staged per wave
     constexpr int MT = LM ? K * K / kBlock : 1;         // multipliers staged per thread
@@ -2403,11 +2403,10 @@ int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &
     if (!kmax) return -1;
     hipStream_t stream = (hipStream_t)L.stream;
     const int64_t ntiles_p = (g.ncols + 63) / 64;   // k_flush_pivot_rows column tiles
-    if (kmax > 96)
+    // (96-slot blocks take the 128-slot form: a 96-slot instance, two blocks
+    // per CU, measured 0.2% slower at config 4, profiles/r04_ab_pivrows96_*.log)
+    if (kmax > 64)
         hipLaunchKernelGGL(k_flush_pivot_rows<128>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
-                           D.Pbuf, D.mul, D.rq);
-    else if (kmax > 64)   // 96 slots: 60 KB of LDS, two blocks per CU (the 128-slot form's 80 KB: one)
-        hipLaunchKernelGGL(k_flush_pivot_rows<96>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
                            D.Pbuf, D.mul, D.rq);
     else
         hipLaunchKernelGGL(k_flush_pivot_rows<64>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
