@@ -2404,7 +2404,7 @@ int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &
     hipStream_t stream = (hipStream_t)L.stream;
     const int64_t ntiles_p = (g.ncols + 63) / 64;   // k_flush_pivot_rows column tiles
     // (96-slot blocks take the 128-slot form: a 96-slot instance, two blocks
-    // per CU, measured 0.2% slower at config 4, profiles/r04_ab_pivrows96_*.log)
+    // per CU, measured 0.2% slower at config 4, profiles/r04_ab_pivrows96.log)
     if (kmax > 64)
         hipLaunchKernelGGL(k_flush_pivot_rows<128>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
                            D.Pbuf, D.mul, D.rq);
