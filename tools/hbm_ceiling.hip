@@ -128,6 +128,58 @@ __global__ __launch_bounds__(256) void k_tile_rmw(double *__restrict__ T, long l
     }
 }
 
+// k_flushw's own access shape without its arithmetic (round 4, layout
+// question): 8-wave blocks over 256-column x IR-row items (column tile
+// fastest), wave tile 16 rows x 32 columns, lane (lk, lc) = column pair 2 lc,
+// rows lk + 4 r, one 16-row band loaded ahead. BLK = 0: row-major with pitch
+// ld; BLK = 1: a blocked layout where every 16-row x 256-column tile is one
+// contiguous 32 KB block (band-major within a column tile), so an item is
+// one contiguous stream.
+template <int BLK>
+__global__ __launch_bounds__(512) void k_wtile_rmw(double *__restrict__ T, long ld, long rows, long live, long ir,
+                                                   double c) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lc = lane & 15, lk = lane >> 4;
+    const long ntiles = (live + 255) / 256, nbands = (rows + 15) / 16;
+    const long nitems = ntiles * ((rows + ir - 1) / ir);
+    const d2 p = {0.5, 0.25};
+    auto addr = [&](long row, long col) -> double * {
+        if (!BLK) return T + row * ld + col;
+        const long t = col >> 8, b = row >> 4;
+        return T + (((t * nbands + b) << 4) + (row & 15)) * 256 + (col & 255);
+    };
+    for (long item = blockIdx.x; item < nitems; item += gridDim.x) {
+        const long tile = item % ntiles, strip = item / ntiles;
+        const long cl = tile * 256 + wave * 32 + 2 * lc;
+        const bool in = cl + 1 < live;
+        const long i0 = strip * ir, i1 = i0 + ir < rows ? i0 + ir : rows;
+        const int nb = (int)((i1 - i0 + 15) / 16);
+        auto tload = [&](d2 (&x)[4], int sb) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const long row = i0 + 16 * sb + lk + 4 * r;
+                x[r] = (in && row < i1) ? __builtin_nontemporal_load((const d2 *)addr(row, cl)) : d2{0.0, 0.0};
+            }
+        };
+        d2 t[4];
+        tload(t, 0);
+        for (int sb = 0; sb < nb; sb++) {
+            d2 tn[4];
+            if (sb + 1 < nb) tload(tn, sb + 1);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const long row = i0 + 16 * sb + lk + 4 * r;
+                d2 x = t[r];
+                x.x = fma(-c, p.x, x.x);
+                x.y = fma(-c, p.y, x.y);
+                if (in && row < i1) __builtin_nontemporal_store(x, (d2 *)addr(row, cl));
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) t[r] = tn[r];
+        }
+    }
+}
+
 typedef void (*TFn)(double *, long, long, long, long, double);
 template <int TW>
 static TFn tile_u(int u) {
@@ -179,6 +231,50 @@ static KFn kernel(int op, int u, bool chunk, bool nt) {
 
 int main(int argc, char **argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 5;
+    if (getenv("LAB_LAYOUT")) {   // the pass's wave-tile shape: pitch paddings and the blocked layout
+        int cus = 0;
+        CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+        const long rows = 16384, live = 32770, ld0 = 49216;
+        const long maxpad = 1024;
+        double *T;
+        const size_t bytes = (size_t)(rows + 16) * (ld0 + maxpad) * 8;
+        CHK(hipMalloc(&T, bytes));
+        CHK(hipMemset(T, 0, bytes));
+        hipEvent_t e0, e1;
+        CHK(hipEventCreate(&e0));
+        CHK(hipEventCreate(&e1));
+        const double moved = 16.0 * rows * live;
+        printf("# layout lab: %ld x %ld live columns, GB/s = bytes read + written / time, best and median of %d\n", rows,
+               live, reps);
+        for (int rep2 = 0; rep2 < 2; rep2++)
+            for (long ir : {1024L, 2048L})
+                for (int blk = 0; blk < 2; blk++)
+                    for (long pad : {0L, 8L, 32L, 64L, 128L, 256L, 512L, 1024L}) {
+                        if (blk && pad) continue;
+                        const long ld = ld0 + pad;
+                        const TFn k = blk ? k_wtile_rmw<1> : k_wtile_rmw<0>;
+                        const int grid = 2 * cus;
+                        hipLaunchKernelGGL(k, dim3(grid), dim3(512), 0, 0, T, ld, rows, live, ir, 1e-3);
+                        CHK(hipDeviceSynchronize());
+                        std::vector<float> t;
+                        for (int r = 0; r < reps; r++) {
+                            CHK(hipEventRecord(e0));
+                            hipLaunchKernelGGL(k, dim3(grid), dim3(512), 0, 0, T, ld, rows, live, ir, 1e-3);
+                            CHK(hipEventRecord(e1));
+                            CHK(hipEventSynchronize(e1));
+                            float ms;
+                            CHK(hipEventElapsedTime(&ms, e0, e1));
+                            t.push_back(ms);
+                        }
+                        std::sort(t.begin(), t.end());
+                        printf("%-9s pitch %6ld (+%4ld) rows/item %5ld : best %7.1f  median %7.1f GB/s  (%.3f ms)\n",
+                               blk ? "blocked" : "row-major", blk ? 0L : ld, pad, ir, moved / t[0] / 1e6,
+                               moved / t[t.size() / 2] / 1e6, t[0]);
+                        fflush(stdout);
+                    }
+        CHK(hipFree(T));
+        return 0;
+    }
     const size_t bytes = (size_t)4 << 30;
     const size_t n = bytes / 16;
     int cus = 0;
