@@ -21,6 +21,7 @@
 // evaluates it for the pivot row, select for columns 0 and k, and k_flush
 // applies it to the whole block of constraint rows in one HBM pass.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace lpg {
