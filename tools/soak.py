@@ -6,7 +6,7 @@ on/off, flush kernel, pricing rule, generator kind, primal / two-phase /
 Big-M / dual). Prints one line per case and a summary; exits 1 on the first
 mismatch (the case's settings are printed so it can be replayed).
 
-    python tools/soak.py [seconds] [seed]
+    python tools/soak.py [seconds] [seed] [big]     (big: m 1024-4097, n 2048-8192)
 """
 import os
 import random
@@ -23,10 +23,14 @@ from oracle.lpo import GEN_ARTIFICIAL, GEN_DEGENERATE, GEN_DENSE, GEN_DUAL, Orac
 KNOBS = ("LPG_DEFER", "LPG_PERSIST", "LPG_NO_REORDER", "LPG_FLUSH_KERNEL", "LPG_PERSIST_WG")
 
 
-def case(rng: random.Random):
+def case(rng: random.Random, big: bool = False):
     mode = rng.choice(["primal", "primal", "primal", "two_phase", "big_m", "dual"])
-    m = rng.choice([16, 33, 64, 100, 255, 256, 257, 300, 511, 512, 700, 1024, 1500])
-    n = rng.choice([16, 48, 100, 257, 500, 1000, 2000, 3000])
+    if big:    # sizes where the pass has many items and the tail, the select grid folds (m % 256 == 0)
+        m = rng.choice([1024, 2047, 2048, 4095, 4096, 4097])
+        n = rng.choice([2048, 6000, 8192])
+    else:
+        m = rng.choice([16, 33, 64, 100, 255, 256, 257, 300, 511, 512, 700, 1024, 1500])
+        n = rng.choice([16, 48, 100, 257, 500, 1000, 2000, 3000])
     env = {
         "LPG_DEFER": str(rng.choice([0, 1, 2, 5, 8, 16, 31, 32, 33, 48, 63, 64, 65, 77, 96, 100, 128])),
         "LPG_PERSIST": rng.choice(["0", "1"]),
@@ -39,7 +43,7 @@ def case(rng: random.Random):
     kind = {"primal": rng.choice([GEN_DENSE, GEN_DEGENERATE]), "two_phase": GEN_ARTIFICIAL,
             "big_m": GEN_ARTIFICIAL, "dual": GEN_DUAL}[mode]
     seed = rng.randrange(1 << 30)
-    cap = rng.choice([50, 200, 1000, 5000])
+    cap = rng.choice([50, 200, 1000]) if big else rng.choice([50, 200, 1000, 5000])
     return dict(mode=mode, m=m, n=n, env=env, rule=rule, kind=kind, seed=seed, cap=cap)
 
 
@@ -92,12 +96,13 @@ def run(c):
 def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 300.0
     seed = int(sys.argv[2]) if len(sys.argv) > 2 else 20261017
+    big = len(sys.argv) > 3 and sys.argv[3] == "big"
     rng = random.Random(seed)
     lpg.load()
     t0 = time.time()
     n = 0
     while time.time() - t0 < budget:
-        c = case(rng)
+        c = case(rng, big)
         try:
             r, bad = run(c)
         except lpg.LPGError as ex:   # a refused combination: reported, not counted as parity
