@@ -368,53 +368,52 @@ int debug_block_phases(unsigned long long *out) {
 #define LPG_BPUB(ph, t) do { } while (0)
 #endif
 
-// The pending chains of one thread, fully unrolled over NS slots with every
-// LDS read issued before the first fma (one wave per SIMD cannot hide an LDS
-// round trip per step). Slots past the chain read as exact no-ops: past q the
-// slices hold +0 and the multiplier / P_u[k] rows hold -0 / +0.
-// Pivot row, column j: x = fma(m_u, P_u[j], x) for u < q; with SEL the steps
-// u <= qs (the row's restart point, uniform) are (-0, +0) no-ops.
-template <int NS, bool SEL>
-__device__ __forceinline__ double chain_row(const double *sPt, const double *wmw, int qs, double x) {
-    d2 pv[NS / 2], mv[NS / 2];
+// The pending chains of one thread over nb batches of 16 slots, software-
+// pipelined: batch b+1's LDS reads are in flight while batch b's 16 dependent
+// fmas run (one wave per SIMD cannot hide an LDS round trip per step; loading
+// all 64 slots before the first fma, round 3's form, held 256 VGPRs of
+// operands and spilled into AGPRs). Slots past the chain read as exact no-ops:
+// past q the slices hold +0 and the multiplier / P_u[k] rows hold -0 / +0, so
+// a step fma(-0, +0, x) is exactly x (and nb = 0 leaves x as it is).
+// Pivot row, column j (ROW): x = fma(m_u, P_u[j], x) for u < q; with SEL the
+// steps u <= lim (the row's restart point, uniform) are (-0, +0) no-ops.
+// Entering column, row i (!ROW): x = fma(-C_v[i], P_v[k], x) for v <= q; with
+// SEL the steps v <= lim (this lane's restart point, -1 if none) are (+0, +0)
+// no-ops. own: this thread's slice slots; uni: the wave's uniform row.
+template <bool ROW, bool SEL>
+__device__ __forceinline__ double chain_batch(const d2 (&o)[8], const d2 (&w)[8], int base, int lim, double x) {
 #pragma unroll
-    for (int j = 0; j < NS / 2; j++) {
-        pv[j] = ((const d2 *)sPt)[j];
-        mv[j] = ((const d2 *)wmw)[j];
-    }
-#pragma unroll
-    for (int j = 0; j < NS / 2; j++) {
-        if (SEL) {
-            const bool l0 = 2 * j > qs, l1 = 2 * j + 1 > qs;
-            x = fma(l0 ? mv[j].x : -0.0, l0 ? pv[j].x : 0.0, x);
-            x = fma(l1 ? mv[j].y : -0.0, l1 ? pv[j].y : 0.0, x);
+    for (int j = 0; j < 8; j++) {
+        const bool l0 = !SEL || base + 2 * j > lim, l1 = !SEL || base + 2 * j + 1 > lim;
+        if (ROW) {
+            x = fma(l0 ? w[j].x : -0.0, l0 ? o[j].x : 0.0, x);
+            x = fma(l1 ? w[j].y : -0.0, l1 ? o[j].y : 0.0, x);
         } else {
-            x = fma(mv[j].x, pv[j].x, x);
-            x = fma(mv[j].y, pv[j].y, x);
+            x = fma(-(l0 ? o[j].x : 0.0), l0 ? w[j].x : 0.0, x);
+            x = fma(-(l1 ? o[j].y : 0.0), l1 ? w[j].y : 0.0, x);
         }
     }
     return x;
 }
-// Entering column, row i: x = fma(-C_v[i], P_v[k], x) for v <= q; with SEL
-// the steps v <= lp (this lane's restart point, -1 if none) are (+0, +0) no-ops.
-template <int NS, bool SEL>
-__device__ __forceinline__ double chain_col(const double *sCt, const double *wpw, int lp, double x) {
-    d2 cv[NS / 2], pk[NS / 2];
+template <bool ROW, bool SEL>
+__device__ __forceinline__ double chain(const double *own, const double *uni, int nb, int lim, double x) {
+    if (nb <= 0) return x;
+    d2 o0[8], w0[8], o1[8], w1[8];
+    auto load = [&](d2 (&o)[8], d2 (&w)[8], int bb) {
 #pragma unroll
-    for (int j = 0; j < NS / 2; j++) {
-        cv[j] = ((const d2 *)sCt)[j];
-        pk[j] = ((const d2 *)wpw)[j];
-    }
-#pragma unroll
-    for (int j = 0; j < NS / 2; j++) {
-        if (SEL) {
-            const bool l0 = 2 * j > lp, l1 = 2 * j + 1 > lp;
-            x = fma(-(l0 ? cv[j].x : 0.0), l0 ? pk[j].x : 0.0, x);
-            x = fma(-(l1 ? cv[j].y : 0.0), l1 ? pk[j].y : 0.0, x);
-        } else {
-            x = fma(-cv[j].x, pk[j].x, x);
-            x = fma(-cv[j].y, pk[j].y, x);
+        for (int j = 0; j < 8; j++) {
+            o[j] = ((const d2 *)own)[8 * bb + j];
+            w[j] = ((const d2 *)uni)[8 * bb + j];
         }
+    };
+    load(o0, w0, 0);
+#pragma unroll 1
+    for (int bb = 0; bb < nb; bb += 2) {
+        if (bb + 1 < nb) load(o1, w1, bb + 1);
+        x = chain_batch<ROW, SEL>(o0, w0, 16 * bb, lim, x);
+        if (bb + 1 >= nb) break;
+        if (bb + 2 < nb) load(o0, w0, bb + 2);
+        x = chain_batch<ROW, SEL>(o1, w1, 16 * (bb + 1), lim, x);
     }
     return x;
 }
@@ -699,15 +698,9 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             if (!on) {
                 // another rank's row: its P slice arrives below
             } else if (qs < 0) {
-                if (q <= 16) x = chain_row<16, false>(sPt, wmw, qs, x);
-                else if (q <= 32) x = chain_row<32, false>(sPt, wmw, qs, x);
-                else if (q <= 48) x = chain_row<48, false>(sPt, wmw, qs, x);
-                else x = chain_row<64, false>(sPt, wmw, qs, x);
+                x = chain<true, false>(sPt, wmw, (q + 15) >> 4, qs, x);      // slots u < q
             } else {
-                if (q <= 16) x = chain_row<16, true>(sPt, wmw, qs, x);
-                else if (q <= 32) x = chain_row<32, true>(sPt, wmw, qs, x);
-                else if (q <= 48) x = chain_row<48, true>(sPt, wmw, qs, x);
-                else x = chain_row<64, true>(sPt, wmw, qs, x);
+                x = chain<true, true>(sPt, wmw, (q + 15) >> 4, qs, x);
             }
             return x;
         };
@@ -1054,24 +1047,15 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             wp[wave][lane] = lane == q ? pkq : pu;
         LPG_BPH(t, 6);
         if (hr) b = (i == rl) ? p0q : fma(-sCt[q], p0q, b);
-        // the chain over slots v <= q (NS > q). A row pivoted earlier in this
+        // the chain over slots v <= q (q / 16 + 1 batches). A row pivoted earlier in this
         // block restarts at its last pivot lp: x = P_lp[k] and the steps up to
         // lp become no-ops (the select form, for waves holding such a row).
         if (hr && lastpiv >= 0) xa = wp[wave][lastpiv];
-        {
+        if (wave * 64 < rw) {                           // waves holding rows (xa is used under hr only)
             const double *wpw = &wp[wave][0];
             const bool sel = __ballot(hr && lastpiv >= 0) != 0ull;
-            if (!sel) {
-                if (q < 16) xa = chain_col<16, false>(sCt, wpw, lastpiv, xa);
-                else if (q < 32) xa = chain_col<32, false>(sCt, wpw, lastpiv, xa);
-                else if (q < 48) xa = chain_col<48, false>(sCt, wpw, lastpiv, xa);
-                else xa = chain_col<64, false>(sCt, wpw, lastpiv, xa);
-            } else {
-                if (q < 16) xa = chain_col<16, true>(sCt, wpw, lastpiv, xa);
-                else if (q < 32) xa = chain_col<32, true>(sCt, wpw, lastpiv, xa);
-                else if (q < 48) xa = chain_col<48, true>(sCt, wpw, lastpiv, xa);
-                else xa = chain_col<64, true>(sCt, wpw, lastpiv, xa);
-            }
+            if (!sel) xa = chain<false, false>(sCt, wpw, (q >> 4) + 1, lastpiv, xa);   // slots v <= q
+            else xa = chain<false, true>(sCt, wpw, (q >> 4) + 1, lastpiv, xa);
         }
         LPG_BPH(t, 7);
         drain();                                        // this pivot's P stores, before the ratio record
