@@ -704,6 +704,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             }
             return x;
         };
+        LPG_BPH(t, 15);
         double x = pivot_row(owns, rloc);
         LPG_BPH(t, 2);
         const uint32_t xt = a.xtag0 + (uint32_t)t;      // MR: this pivot's exchange tag

@@ -30,12 +30,13 @@ torch.cuda.synchronize()
 NS = 16                              # stamp slots per pivot (lpg_block.hip g_bph)
 buf = (ctypes.c_ulonglong * (2 * 64 * NS + 2 * 64 * 256))()
 assert lib.lpg_debug_block_phases(buf) == 0
-# stamp ids in time order within a pivot: 0 top, 1 ratio decision known, 2 pivot row (loads + chain),
+# stamp ids in time order within a pivot: 0 top, 1 ratio decision known, 15 pivot row loaded, 2 its chain,
 # 8 bookkeeping done, 9 drain, 10 P / d / pricing computed, 11 slice argmin, 3 pricing record published,
 # 4 pricing decision known, 6 column loads in, 7 column chain, 12 drain, 13 C / ratio candidate,
 # 14 slice argmin, 5 ratio record published; then the next pivot's 0
-order = [0, 1, 2, 8, 9, 10, 11, 3, 4, 6, 7, 12, 13, 14, 5]
-names = ["P-sweep", "row-load+chain", "bookkeeping", "P-drain", "P/d/price", "P-argmin", "P-store",
+# (15: the pivot row's loads landed and the barrier passed, before its chain)
+order = [0, 1, 15, 2, 8, 9, 10, 11, 3, 4, 6, 7, 12, 13, 14, 5]
+names = ["P-sweep", "row-load", "row-chain", "bookkeeping", "P-drain", "P/d/price", "P-argmin", "P-store",
          "S-sweep", "S-load", "S-chain", "S-drain", "C/cand", "S-argmin", "S-store", "->next"]
 for w in (0, 1):
     st = [[buf[(w * 64 + t) * NS + k] for k in range(NS)] for t in range(K)]
