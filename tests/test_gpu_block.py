@@ -92,6 +92,23 @@ def test_to_optimality(lpg, monkeypatch, wg, defer, m, n, seed, kind, rule, trad
     _assert_same(e, o, m)
 
 
+@pytest.mark.parametrize("defer", [15, 16, 17, 31, 33, 47, 48, 49, 63])
+@pytest.mark.parametrize("m,n,seed,kind,rule", [(300, 450, 21, 0, 0), (257, 300, 22, 1, 1)])
+def test_chain_batch_edges(lpg, monkeypatch, defer, m, n, seed, kind, rule):
+    """The chains run in batches of 16 slots (lpg_block.hip chain<>): block
+    sizes on either side of every batch edge, dense (Dantzig) and degenerate
+    (Bland: pivot rows that recur inside a block take the restart form)."""
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer)
+    assert e.info.pivot_wg > 0
+    o = Oracle(m, n + m + 1)
+    e.generate(n, seed, kind)
+    o.generate(n, seed, kind)
+    res = e.solve(200_000, rule)
+    ores = o.solve(200_000, rule)
+    assert res.status == ores.status and res.pivots == ores.pivots > 2 * defer
+    _assert_same(e, o, m)
+
+
 @pytest.mark.parametrize("wg", [None, 17])
 def test_config2_to_optimality(lpg, monkeypatch, wg):
     m, n = 1024, 2048
