@@ -348,11 +348,14 @@ __device__ unsigned long long g_bph[2][64][16];
 #else                      // completion stamps: everything issued so far has landed
 #define LPG_BPH_WAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
 #endif
+__device__ unsigned long long g_bclk[64];   // shader clock (clock64) beside workgroup 0's stamp 0
 #define LPG_BPH(t, k)                                                                          \
     do {                                                                                       \
         LPG_BPH_WAIT();                                                                        \
-        if (tid == 0 && (wg == 0 || wg == nwg / 2) && (t) < 64)                                \
+        if (tid == 0 && (wg == 0 || wg == nwg / 2) && (t) < 64) {                              \
             g_bph[wg == 0 ? 0 : 1][(t)][(k)] = __builtin_amdgcn_s_memrealtime();               \
+            if ((k) == 0 && wg == 0) g_bclk[(t)] = clock64();                                  \
+        }                                                                                      \
     } while (0)
 __device__ unsigned long long g_bpub[2][64][256];   // every workgroup's publish stamp, phase P / S
 #define LPG_BPUB(ph, t)                                                                        \
@@ -361,7 +364,10 @@ __device__ unsigned long long g_bpub[2][64][256];   // every workgroup's publish
     } while (0)
 int debug_block_phases(unsigned long long *out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bph), sizeof g_bph) != hipSuccess) return -1;
-    return hipMemcpyFromSymbol(out + sizeof g_bph / 8, HIP_SYMBOL(g_bpub), sizeof g_bpub) == hipSuccess ? 0 : -1;
+    if (hipMemcpyFromSymbol(out + sizeof g_bph / 8, HIP_SYMBOL(g_bpub), sizeof g_bpub) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out + (sizeof g_bph + sizeof g_bpub) / 8, HIP_SYMBOL(g_bclk), sizeof g_bclk) == hipSuccess
+               ? 0
+               : -1;
 }
 #else
 #define LPG_BPH(t, k) do { } while (0)
@@ -395,27 +401,39 @@ __device__ __forceinline__ double chain_batch(const d2 (&o)[8], const d2 (&w)[8]
     }
     return x;
 }
-template <bool ROW, bool SEL>
-__device__ __forceinline__ double chain(const double *own, const double *uni, int nb, int lim, double x) {
-    if (nb <= 0) return x;
-    d2 o0[8], w0[8], o1[8], w1[8];
-    auto load = [&](d2 (&o)[8], d2 (&w)[8], int bb) {
+// NB batches, fully unrolled: batch b+1's reads are issued before batch b's
+// fmas (a runtime loop over the batches measured slower from the third batch
+// on: its back-edge carried the prefetched operands through spills)
+template <bool ROW, bool SEL, int NB>
+__device__ __forceinline__ double chain_n(const double *own, const double *uni, int lim, double x) {
+    d2 o[2][8], w[2][8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            o[j] = ((const d2 *)own)[8 * bb + j];
-            w[j] = ((const d2 *)uni)[8 * bb + j];
+    for (int j = 0; j < 8; j++) {
+        o[0][j] = ((const d2 *)own)[j];
+        w[0][j] = ((const d2 *)uni)[j];
+    }
+#pragma unroll
+    for (int bb = 0; bb < NB; bb++) {
+        if (bb + 1 < NB) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                o[(bb + 1) & 1][j] = ((const d2 *)own)[8 * (bb + 1) + j];
+                w[(bb + 1) & 1][j] = ((const d2 *)uni)[8 * (bb + 1) + j];
+            }
         }
-    };
-    load(o0, w0, 0);
-#pragma unroll 1
-    for (int bb = 0; bb < nb; bb += 2) {
-        if (bb + 1 < nb) load(o1, w1, bb + 1);
-        x = chain_batch<ROW, SEL>(o0, w0, 16 * bb, lim, x);
-        if (bb + 1 >= nb) break;
-        if (bb + 2 < nb) load(o0, w0, bb + 2);
-        x = chain_batch<ROW, SEL>(o1, w1, 16 * (bb + 1), lim, x);
+        x = chain_batch<ROW, SEL>(o[bb & 1], w[bb & 1], 16 * bb, lim, x);
     }
     return x;
+}
+template <bool ROW, bool SEL>
+__device__ __forceinline__ double chain(const double *own, const double *uni, int nb, int lim, double x) {
+    switch (nb) {      // nb <= 4: blocks of <= 64 pivots (block_geometry)
+        case 0: return x;
+        case 1: return chain_n<ROW, SEL, 1>(own, uni, lim, x);
+        case 2: return chain_n<ROW, SEL, 2>(own, uni, lim, x);
+        case 3: return chain_n<ROW, SEL, 3>(own, uni, lim, x);
+        default: return chain_n<ROW, SEL, 4>(own, uni, lim, x);
+    }
 }
 
 struct BlockArgs {

@@ -28,7 +28,7 @@ e.solve(2 * K, 0)                    # warm: bootstrap + two blocks, flushed
 e.enqueue(K, 0)                      # one launch of K pivots
 torch.cuda.synchronize()
 NS = 16                              # stamp slots per pivot (lpg_block.hip g_bph)
-buf = (ctypes.c_ulonglong * (2 * 64 * NS + 2 * 64 * 256))()
+buf = (ctypes.c_ulonglong * (2 * 64 * NS + 2 * 64 * 256 + 64))()   # + workgroup 0's clock64 beside stamp 0
 assert lib.lpg_debug_block_phases(buf) == 0
 # stamp ids in time order within a pivot: 0 top, 1 ratio decision known, 15 pivot row loaded, 2 its chain,
 # 8 bookkeeping done, 9 drain, 10 P / d / pricing computed, 11 slice argmin, 3 pricing record published,
@@ -69,3 +69,9 @@ for ph, nm in ((0, "P"), (1, "S")):
     print(f"phase {nm} publish: max-median {statistics.mean(a for a, _ in spread):.2f} us, "
           f"median-min {statistics.mean(b for _, b in spread):.2f} us; latest workgroups: "
           + ", ".join(f"{w}x{c}" for w, c in sorted(late.items(), key=lambda x: -x[1])[:8]))
+
+# shader clock over the launch: clock64 ticks / s_memrealtime (100 MHz) ticks
+clk = [buf[2 * 64 * NS + 2 * 64 * 256 + t] for t in range(K)]
+st0 = [buf[t * NS] for t in range(K)]
+if K > 2 and st0[K - 1] > st0[1]:
+    print(f"shader clock over pivots 1..{K - 1}: {(clk[K - 1] - clk[1]) / ((st0[K - 1] - st0[1]) * 10.0):.3f} GHz (clock64 / s_memrealtime)")

@@ -77,10 +77,13 @@ __global__ __launch_bounds__(256, 1) void k_chain_lab(double *out, unsigned long
     __syncthreads();
     double x = 1.0 + tid;
     const int nb = (q + 15) >> 4;
-    unsigned long long t0 = 0;
+    unsigned long long t0 = 0, c0 = 0;
     for (int r = 0; r < kReps; r++) {
         __syncthreads();
-        if (r == 1 && tid == 0) t0 = __builtin_amdgcn_s_memrealtime();
+        if (r == 1 && tid == 0) {
+            t0 = __builtin_amdgcn_s_memrealtime();
+            c0 = clock64();
+        }
         if (FORM == 0) {
             x = chain<true, false>(sPt, &wm[wave][0], nb, -1, x);
         } else if (FORM == 3) {                  // the uniform operand by readlane (lane u holds slot u)
@@ -102,9 +105,14 @@ __global__ __launch_bounds__(256, 1) void k_chain_lab(double *out, unsigned long
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) ticks[blockIdx.x] = __builtin_amdgcn_s_memrealtime() - t0;
+    if (tid == 0) {
+        ticks[blockIdx.x] = __builtin_amdgcn_s_memrealtime() - t0;
+        ticks[kNWG + blockIdx.x] = clock64() - c0;
+    }
     out[(size_t)blockIdx.x * 256 + tid] = x;
 }
+
+double g_ghz = 0;   // shader clock of the last run (clock64 / s_memrealtime)
 
 template <int FORM>
 double run(double *out, unsigned long long *ticks, int q) {
@@ -114,10 +122,11 @@ double run(double *out, unsigned long long *ticks, int q) {
     (void)hipDeviceSynchronize();
     hipLaunchKernelGGL(k_chain_lab<FORM>, dim3(kNWG), dim3(256), lds, 0, out, ticks, q);
     (void)hipDeviceSynchronize();
-    unsigned long long h[kNWG];
+    unsigned long long h[2 * kNWG];
     (void)hipMemcpy(h, ticks, sizeof h, hipMemcpyDeviceToHost);
-    double s = 0;
-    for (int w = 0; w < kNWG; w++) s += (double)h[w];
+    double s = 0, c = 0;
+    for (int w = 0; w < kNWG; w++) s += (double)h[w], c += (double)h[kNWG + w];
+    g_ghz = c / (s * 10.0);
     return s / kNWG * 10.0 / (kReps - 1);   // ns per run
 }
 }  // namespace
@@ -126,15 +135,17 @@ int main() {
     double *out;
     unsigned long long *ticks;
     if (hipMalloc(&out, (size_t)kNWG * 256 * sizeof(double)) != hipSuccess ||
-        hipMalloc(&ticks, kNWG * sizeof(unsigned long long)) != hipSuccess)
+        hipMalloc(&ticks, 2 * kNWG * sizeof(unsigned long long)) != hipSuccess)
         return 1;
     printf("# chain lab: %d workgroups x 256 threads, %d columns per slice, stride %d; ns per chain run (mean over workgroups)\n",
            kNWG, kCW, kS);
     for (int q : {8, 16, 24, 32, 40, 48, 56, 64}) {
-        const double a = run<0>(out, ticks, q), b = run<1>(out, ticks, q), c = run<2>(out, ticks, q);
+        const double a = run<0>(out, ticks, q);
+        const double ghz = g_ghz;
+        const double b = run<1>(out, ticks, q), c = run<2>(out, ticks, q);
         const double d = run<3>(out, ticks, q);
-        printf("q=%2d batches=%d  chain %7.1f ns   readlane chain %7.1f ns   LDS reads only %7.1f ns   fmas only %7.1f ns\n",
-               q, (q + 15) >> 4, a, d, b, c);
+        printf("q=%2d batches=%d  chain %7.1f ns (%.2f GHz)   readlane chain %7.1f ns   LDS reads only %7.1f ns   fmas only %7.1f ns\n",
+               q, (q + 15) >> 4, a, ghz, d, b, c);
     }
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
