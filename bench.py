@@ -59,6 +59,44 @@ CONFIGS = {
 }
 
 
+def source_stamp() -> str:
+    """Hash of the engine's sources (csrc/*.hip, csrc/*.h, include/lpg.h): a PMC
+    traffic file is attached only to a bench line of the build it measured."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "linearprogramming_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "linearprogramming_amd", "csrc", "*.h")) +
+                   [os.path.join(ROOT, "include", "lpg.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(a, kname, defer, m, n, world, stamp):
+    """The PMC traffic of profiles/pmc_config{C}.json, or None and the reason:
+    the file must carry this build's source stamp and this run's kernel,
+    pending-pivot count and LP shape (a stand-in
+    --shape run or a changed pass never inherits a stale figure)."""
+    pmc = os.path.join(ROOT, "profiles", f"pmc_config{a.config}.json")
+    if not defer:
+        return None, "eager updates: no PMC file"
+    if world != 1 or a.shape:
+        return None, "PMC files are captured for the single-GPU BASELINE configs only"
+    if not os.path.exists(pmc):
+        return None, f"no {os.path.relpath(pmc, ROOT)}"
+    with open(pmc) as f:
+        p = json.load(f)
+    want = {"kernel": kname, "pending_pivots": defer, "m": m, "n": n, "source_stamp": stamp}
+    diff = {k: (p.get(k), v) for k, v in want.items() if p.get(k) != v}
+    if diff:
+        return None, (f"{os.path.relpath(pmc, ROOT)} does not match this run (field: file vs run): "
+                      + ", ".join(f"{k}: {x!r} vs {y!r}" for k, (x, y) in diff.items()))
+    return p, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -388,14 +426,15 @@ def main():
         roof.update({"ms_per_block": ms_block, "other_ms_per_block": other_ms,
                      "block_ceiling_ms": ceil_ms, "block_ceiling_pivots_per_s": defer / (ceil_ms * 1e-3),
                      "pass_only_ceiling_pivots_per_s": defer / (touched / (HBM_PEAK_GBS * 1e9))})
-    pmc = os.path.join(ROOT, "profiles", f"pmc_config{a.config}.json")
-    if os.path.exists(pmc) and defer:
-        with open(pmc) as f:
-            p = json.load(f)
-        if p.get("kernel") == kname and p.get("pending_pivots") == defer and world == 1:
-            roof["traffic"] = p.get("hbm_bytes_per_launch")
-            roof["traffic_source"] = (f"static: {os.path.relpath(pmc, ROOT)} (separate rocprofv3 --pmc passes of this "
-                                      f"bench, {kname}, {defer} pending pivots)")
+    stamp = source_stamp()
+    roof["source_stamp"] = stamp
+    p, why = pmc_traffic(a, kname, defer, m, n, world, stamp)
+    if p is not None:
+        roof["traffic"] = p.get("hbm_bytes_per_launch")
+        roof["traffic_source"] = (f"profiles/pmc_config{a.config}.json: separate rocprofv3 --pmc FETCH_SIZE / "
+                                  f"WRITE_SIZE passes of this bench at source stamp {stamp} ({p.get('source')})")
+    else:
+        roof["traffic_note"] = why
     line = {
         "metric": METRIC,
         "value": done / elapsed,

@@ -176,7 +176,13 @@ int  lpg_comm_init_host(lpg_ctx *ctx, const lpg_host_comm_ops *ops);
  * blocks of <= 64 pivots run as one persistent launch per block on every
  * rank (lpg_info.pivot_wg > 0; each rank needs its own GPU, or launches
  * small enough to be resident together; env LPG_PERSIST_MR=0: two kernels
- * per pivot). */
+ * per pivot). The exchange's kernels spin-wait on their peers, so attaching
+ * is refused (LPG_ERR_STATE, lpg_last_error names the reason) when ranks
+ * would depend on each other for hardware queues or CUs: ranks that are
+ * threads of one process (lpg_comm_init_push_local, world > 1), or ranks of
+ * several processes on one GPU (same PCI bus id). Nothing has pivoted then:
+ * the caller keeps the collectives. Env LPG_PUSH_SHARED_QUEUES=1 /
+ * LPG_PUSH_SHARED_DEVICE=1 acknowledge the sharing (tests on one GPU). */
 #define LPG_PUSH_HANDLE_BYTES 64
 int  lpg_comm_push_handle(lpg_ctx *ctx, void *handle, size_t len);
 int  lpg_comm_push_base(lpg_ctx *ctx, void **base);

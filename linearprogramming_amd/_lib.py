@@ -177,6 +177,29 @@ def duplicated_libraries() -> dict:
     return {k: v for k, v in fam.items() if len(v) > 1}
 
 
+TESTHOOKS_PATH = os.path.join(_HERE, "liblpg_testhooks.so")
+_private = {}
+
+
+def load_testhooks(path: str = TESTHOOKS_PATH) -> ctypes.CDLL:
+    """The engine built with its test-only fault hooks (LPG_TEST_HOOKS, the
+    Makefile's liblpg_testhooks.so), loaded privately (RTLD_LOCAL, linked
+    -Bsymbolic) next to liblpg.so for the tests that need a hook; pass it to
+    Engine(lib=...). The product library has no hook."""
+    if path in _private:
+        return _private[path]
+    if not os.path.exists(path):
+        raise RuntimeError(f"test-hook engine not built: {path} is missing (run `make`)")
+    bind_runtime()
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    for name, res, args in PROTOTYPES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _private[path] = lib
+    return lib
+
+
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
     """Load liblpg.so and declare every prototype. Raises if it is absent."""
     global _lib

@@ -10,6 +10,7 @@
 #include <rccl/rccl.h>   // types only: RCCL itself is opened at the first communicator (rccl_api())
 
 #include <dlfcn.h>
+#include <unistd.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -113,9 +114,14 @@ struct lpg_ctx {
     int64_t cs = 0;
     int64_t *rq = nullptr;
     int skip = 1;                 // column skipping in the update (LPG_FLAG_NO_SKIP turns it off)
-    // tests only (LPG_TEST_PENDING_FAULT=F:W): before flush F, make the pending
-    // block inconsistent (W = npend | kq | lv | rq) to exercise k_swap_plan's guard
+    // the test-hook build only (LPG_TEST_HOOKS; env LPG_TEST_PENDING_FAULT=F:W):
+    // before flush F, make the pending block inconsistent (W = npend | kq | lv |
+    // rq | ahead) to exercise k_swap_plan's guard
     int inject_flush = -1, inject_what = 0;
+    // k_swap_plan refused a pending block (pending_fault): the basis already
+    // holds the block's pivots while the constraint rows do not, so every
+    // pivoting entry point refuses until the LP is reloaded or regenerated
+    bool poisoned = false;
     int64_t nflush = 0;           // flush_launch calls so far
     unsigned long long touched_mark = 0;
     // communication
@@ -331,23 +337,38 @@ static bool reorders(const lpg_ctx *c) { return c->defer_k > 0 && c->fast_pivot 
 // The timing ring brackets the block pass alone (k_flushw / k_flushm), the
 // kernel the roofline reports; the swap plan, pivot-row rewrite and column
 // swaps around it count as "other" time per pivot.
+#ifdef LPG_TEST_HOOKS
 // The test hook's corruptions, one hipMemsetAsync each: npend = 0x7f7f.. (far
 // above any block), kq[0] = lv[0] = -1 (no column), rq[0] = 0x7f7f.. (no row).
+// "ahead" (5): npend one past the slots the block filled (what a block stopped
+// mid-way can leave), so the plan meets a slot no pivot of this block wrote.
 static int inject_pending_fault(lpg_ctx *c) {
     switch (c->inject_what) {
         case 1: HIPCHK(c, hipMemsetAsync(&c->st->npend, 0x7f, sizeof(int64_t), c->stream)); break;
         case 2: HIPCHK(c, hipMemsetAsync(c->kq, 0xff, sizeof(int64_t), c->stream)); break;
         case 3: HIPCHK(c, hipMemsetAsync(c->lv, 0xff, sizeof(int64_t), c->stream)); break;
         case 4: HIPCHK(c, hipMemsetAsync(c->rq, 0x7f, sizeof(int64_t), c->stream)); break;
+        case 5: {
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            int64_t np = 0;
+            HIPCHK(c, hipMemcpy(&np, &c->st->npend, sizeof np, hipMemcpyDeviceToHost));
+            np += 1;
+            HIPCHK(c, hipMemcpy(&c->st->npend, &np, sizeof np, hipMemcpyHostToDevice));
+            break;
+        }
         default: break;
     }
     return 0;
 }
 
+#endif
+
 static int flush_launch(lpg_ctx *c) {
     int rc;
     const bool re = reorders(c);
+#ifdef LPG_TEST_HOOKS
     if (c->inject_flush >= 0 && c->nflush == c->inject_flush && (rc = inject_pending_fault(c))) return rc;
+#endif
     c->nflush++;
     if (launch_swap_plan(lau(c), geo(c), c->st, defer_of(c, 0), c->colmap, c->inv, c->pairs, re ? 1 : 0, c->defer_k) ||
         (re && launch_move_cols(lau(c), geo(c), c->st, defer_of(c, 0), c->pairs)))
@@ -359,7 +380,9 @@ static int flush_launch(lpg_ctx *c) {
     if (launch_flush_tail(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, !re))
         return fail(c, LPG_ERR_DEVICE, "flush launch failed");
     if (re) {   // k_fill_cols also clears the pending block
-        if (launch_fill_cols(lau(c), geo(c), c->pairs, c->st)) return fail(c, LPG_ERR_DEVICE, "fill launch failed");
+        const Defer D = defer_of(c, 0);
+        if (launch_fill_cols(lau(c), geo(c), c->pairs, c->st, &D, flush_kmax_supported(c->defer_k)))
+            return fail(c, LPG_ERR_DEVICE, "fill launch failed");
         c->permuted = true;
     }
     c->pend = 0;
@@ -725,10 +748,21 @@ static int recover_residency(lpg_ctx *c, const DevState &h) {
 static int pending_fault(lpg_ctx *c, const DevState &h) {
     static const char *const what[] = {"?", "npend", "kq", "lv", "rq"};
     const int64_t w = h.stall_info[0] >= 1 && h.stall_info[0] <= 4 ? h.stall_info[0] : 0;
+    c->poisoned = true;   // the basis holds the block's pivots, the constraint rows do not
     return fail(c, LPG_ERR_STATE,
                 "pending block inconsistent at the flush (%s[%lld] = %lld, npend %lld): the loop was stopped with "
                 "NUMERIC instead of indexing with it; the constraint rows were not brought up to date",
                 what[w], (long long)h.stall_info[1], (long long)h.stall_info[2], (long long)h.stall_info[3]);
+}
+
+// Every pivoting entry point: a context whose pending block was refused
+// (pending_fault) stays refused until lpg_load_rows / lpg_generate rewrite
+// the tableau (continuing would pivot on a basis and constraint
+// rows that disagree).
+static int usable(lpg_ctx *c) {
+    if (!c->poisoned) return 0;
+    return fail(c, LPG_ERR_STATE, "context unusable: an earlier flush refused an inconsistent pending block, so the "
+                "basis and the constraint rows disagree; reload (lpg_load_rows) or regenerate (lpg_generate) the LP");
 }
 
 static int read_result(lpg_ctx *c, lpg_result *out, int rule) {
@@ -885,16 +919,20 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->no_reorder = nr ? atoi(nr) != 0 : (world == 1 && tbytes < 2e9);
     const char *sp = getenv("LPG_SLOW_PIVOT");
     c->fast_pivot = !(sp && atoi(sp));
+#ifdef LPG_TEST_HOOKS
+    // the test-hook build only (linearprogramming_amd/liblpg_testhooks.so,
+    // Makefile): the product library never reads this variable
     if (const char *pf = getenv("LPG_TEST_PENDING_FAULT")) {
         char w[16] = {0};
         int f = -1;
         if (sscanf(pf, "%d:%15s", &f, w) == 2) {
-            static const char *const names[] = {"", "npend", "kq", "lv", "rq"};
-            for (int u = 1; u <= 4; u++)
+            static const char *const names[] = {"", "npend", "kq", "lv", "rq", "ahead"};
+            for (int u = 1; u <= 5; u++)
                 if (!strcmp(w, names[u])) c->inject_what = u;
             c->inject_flush = c->inject_what ? f : -1;
         }
     }
+#endif
     const char *fv = getenv("LPG_FLUSH_KERNEL");   // m | w: force k_flushm / k_flushw (tests); default by block size
     c->flush_variant = fv ? (fv[0] == 'w' ? 1 : fv[0] == 'm' ? 0 : -1) : -1;
     int rc;
@@ -981,11 +1019,12 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         (c->Cbuf && hipMemset(c->Cbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->cs * sizeof(double)) != hipSuccess) ||
         (c->Pbuf && hipMemset(c->Pbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->ld * sizeof(double)) != hipSuccess) ||
         (c->zrow && hipMemset(c->zrow, 0, (size_t)c->ld * sizeof(double)) != hipSuccess) ||
-        // slots a stopped block never filled read as out of range (kq = lv = 0,
-        // rq = -1 is a non-owner row), which k_swap_plan refuses
+        // slots no pivot of the current block filled read as out of range
+        // (kq = lv = 0: no column; rq 0x8080.. < -1: no row), which k_swap_plan
+        // refuses; every block's end writes the same sentinels back (end_block)
         (c->kq && hipMemset(c->kq, 0, (size_t)flush_kmax_supported(c->defer_k) * sizeof(int64_t)) != hipSuccess) ||
         (c->lv && hipMemset(c->lv, 0, (size_t)flush_kmax_supported(c->defer_k) * sizeof(int64_t)) != hipSuccess) ||
-        (c->rq && hipMemset(c->rq, 0xff, (size_t)flush_kmax_supported(c->defer_k) * sizeof(int64_t)) != hipSuccess) ||
+        (c->rq && hipMemset(c->rq, 0x80, (size_t)flush_kmax_supported(c->defer_k) * sizeof(int64_t)) != hipSuccess) ||
         (c->pv && hipMemset(c->pv, 0, (size_t)flush_kmax_supported(c->defer_k) * sizeof(double)) != hipSuccess) ||
         (c->rec && hipMemset(c->rec, 0, (size_t)block_records_bytes(c->pb_nwg)) != hipSuccess) ||
         (c->colmap && (launch_iota(lau(c), c->colmap, c->ld) || launch_iota(lau(c), c->inv, c->ld)))) {
@@ -1079,6 +1118,51 @@ static int ensure_xbuf(lpg_ctx *c) {
     }
     c->xbuf = (char *)p;
     HIPCHK(c, hipMemset(c->xbuf, 0, (size_t)c->xbytes));
+    // identity of the GPU this buffer lives on, read by every peer at attach
+    // (push_shares_device): PCI bus id, then the owning process id
+    char id[kXchIdBytes] = {0};
+    HIPCHK(c, hipDeviceGetPCIBusId(id, 48, c->device));
+    const int32_t pid = (int32_t)getpid();
+    memcpy(id + 48, &pid, sizeof pid);
+    HIPCHK(c, hipMemcpy(c->xbuf + c->xoffG + kXchIdOff, id, sizeof id, hipMemcpyHostToDevice));
+    return 0;
+}
+
+// the push's kernels spin-wait on a peer's kernel, so
+// two ranks must never depend on each other for CUs or hardware queues. Two
+// refusals at attach time, each with a named error, instead of a 2 s
+// exchange timeout in the middle of a solve:
+//  * ranks of ONE process (lpg_comm_init_push_local, world > 1) share its
+//    hardware queues (GPU_MAX_HW_QUEUES): a rank's waiting kernel can sit in
+//    front of the peer kernel it waits for (tools/soak_dist.py measured 108
+//    such timeouts in 784 cases with 4 queues, 14 in 2,721 with 16);
+//  * ranks of several processes on ONE GPU (the same PCI bus id in their
+//    exchange buffers) share its CUs: a non-owner's spinning grid can hold
+//    the CUs the owner's grid needs.
+// The deployment layout (one process per GPU: bench.py under
+// torch.distributed, lpgcli --gpus P on a P-GPU node) passes both checks.
+// Tests that exercise the protocol on the one GPU of this pool, at sizes
+// whose grids co-reside, acknowledge the sharing with LPG_PUSH_SHARED_QUEUES=1
+// / LPG_PUSH_SHARED_DEVICE=1.
+static bool env_on(const char *name) {
+    const char *v = getenv(name);
+    return v && atoi(v) != 0;
+}
+
+static int push_shares_device(lpg_ctx *c, const std::vector<char *> &bases) {
+    if (env_on("LPG_PUSH_SHARED_DEVICE")) return 0;
+    char mine[kXchIdBytes], peer[kXchIdBytes];
+    HIPCHK(c, hipMemcpy(mine, c->xbuf + c->xoffG + kXchIdOff, sizeof mine, hipMemcpyDeviceToHost));
+    for (int r = 0; r < c->world; r++) {
+        if (r == c->rank) continue;
+        HIPCHK(c, hipMemcpy(peer, bases[r] + c->xoffG + kXchIdOff, sizeof peer, hipMemcpyDeviceToHost));
+        if (peer[0] && !strncmp(mine, peer, 48))
+            return fail(c, LPG_ERR_STATE,
+                        "owner-push exchange refused: ranks %d and %d share GPU %.48s, so a rank's spin-waiting "
+                        "exchange kernel can hold the CUs its peer needs; use one GPU per rank, or the collectives "
+                        "(LPG_PUSH_SHARED_DEVICE=1 acknowledges the sharing for small co-resident tests)",
+                        c->rank, r, mine);
+    }
     return 0;
 }
 
@@ -1134,6 +1218,11 @@ int lpg_comm_init_push(lpg_ctx *c, const void *handles, size_t len) {
         c->xpeer.push_back(p);
         bases[r] = (char *)p;
     }
+    if ((rc = push_shares_device(c, bases))) {
+        for (void *p : c->xpeer) (void)hipIpcCloseMemHandle(p);
+        c->xpeer.clear();
+        return rc;
+    }
     return attach_push(c, bases);
 }
 
@@ -1143,6 +1232,12 @@ int lpg_comm_init_push_local(lpg_ctx *c, void *const *bases_in, int world) {
     int rc;
     if ((rc = use_device(c)) || (rc = ensure_xbuf(c))) return rc;
     if (bases_in[c->rank] != c->xbuf) return fail(c, LPG_ERR_ARG, "bases[rank] is not this rank's buffer");
+    if (world > 1 && !env_on("LPG_PUSH_SHARED_QUEUES"))
+        return fail(c, LPG_ERR_STATE,
+                    "owner-push exchange refused: the %d ranks are threads of one process and share its hardware "
+                    "queues, so a rank's spin-waiting exchange kernel can sit in front of the peer kernel it waits "
+                    "for; use one process per GPU, or the collectives (LPG_PUSH_SHARED_QUEUES=1 acknowledges the "
+                    "sharing for tests)", world);
     std::vector<char *> bases((size_t)world);
     for (int r = 0; r < world; r++) bases[r] = (char *)bases_in[r];
     return attach_push(c, bases);
@@ -1209,6 +1304,7 @@ int lpg_load_rows(lpg_ctx *c, int64_t row0, int64_t nrows, const double *rows, i
             HIPCHK(c, hipMemcpy(c->T + (c->nloc + q) * c->ld, rows + (gi - row0) * ld, c->ncols * sizeof(double),
                                 hipMemcpyHostToDevice));
     }
+    c->poisoned = false;   // the caller rewrites the tableau (its pending block was cleared at the refusal)
     return reset_state(c);
 }
 
@@ -1297,6 +1393,7 @@ int lpg_generate(lpg_ctx *c, int64_t n, uint64_t seed, int kind) {
     c->permuted = false;
     c->pend = 0;                 // the generator overwrites the whole tableau: nothing pending survives
     if (launch_generate(lau(c), geo(c), n, seed, kind, c->basis)) return fail(c, LPG_ERR_DEVICE, "generate launch failed");
+    c->poisoned = false;   // the whole tableau and the basis are rewritten
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return reset_state(c);
 }
@@ -1306,6 +1403,7 @@ int lpg_enqueue(lpg_ctx *c, int64_t npiv, int rule) {
         return fail(c, LPG_ERR_ARG, "lpg_enqueue: bad arguments");
     int rc;
     if ((rc = use_device(c))) return rc;
+    if ((rc = usable(c))) return rc;
     if ((rc = ensure_log(c, c->enq + npiv))) return rc;
     return enqueue(c, npiv, rule);
 }
@@ -1320,6 +1418,7 @@ int lpg_reserve_log(lpg_ctx *c, int64_t npivots) {
 int lpg_prepare(lpg_ctx *c, int rule) {
     if (!c || (rule != LPG_RULE_DANTZIG && rule != LPG_RULE_BLAND)) return fail(c, LPG_ERR_ARG, "lpg_prepare: bad arguments");
     int rc;
+    if ((rc = usable(c))) return rc;
     if ((rc = use_device(c)) || (rc = materialize(c))) return rc;
     if (!c->booted || c->boot_rule != rule)
         if ((rc = bootstrap(c, rule))) return rc;
@@ -1362,6 +1461,7 @@ int lpg_solve(lpg_ctx *c, int64_t max_pivots, int rule, lpg_result *out) {
         return fail(c, LPG_ERR_ARG, "lpg_solve: bad arguments");
     int rc;
     if ((rc = use_device(c))) return rc;
+    if ((rc = usable(c))) return rc;
     lpg_result r;
     if (c->booted && c->boot_rule == rule) {
         if ((rc = read_result(c, &r, rule))) return rc;
@@ -1396,6 +1496,7 @@ int lpg_pivot(lpg_ctx *c, int64_t k, int64_t r) {
     if (!c || k < 1 || k >= c->ncols || r < 0 || r >= c->m) return fail(c, LPG_ERR_ARG, "lpg_pivot: bad (k, r)");
     int rc;
     if ((rc = use_device(c))) return rc;
+    if ((rc = usable(c))) return rc;
     if ((rc = ensure_log(c, c->enq + 1))) return rc;
     const int rule = c->booted ? c->boot_rule : LPG_RULE_DANTZIG;
     lpg_result before, after;
@@ -1450,6 +1551,7 @@ int lpg_solve_two_phase(lpg_ctx *c, int64_t art_first, const double *cost, int64
     if (c->world > 1 && !has_comm(c)) return fail(c, LPG_ERR_STATE, "lpg_solve_two_phase: no communicator attached");
     int rc;
     if ((rc = use_device(c))) return rc;
+    if ((rc = usable(c))) return rc;
     const int64_t N = c->ncols - 1;
     std::vector<double> own;
     if (!cost) {   // costs = -1 x the objective row as loaded (slack-form -c row, replicated)
@@ -1515,6 +1617,7 @@ int lpg_solve_big_m(lpg_ctx *c, int64_t art_first, const double *cost, int64_t m
         return fail(c, LPG_ERR_ARG, "lpg_solve_big_m: bad arguments");
     if (c->nobj != 2) return fail(c, LPG_ERR_STATE, "lpg_solve_big_m needs a context created with LPG_FLAG_BIG_M");
     int rc;
+    if ((rc = usable(c))) return rc;
     if ((rc = use_device(c))) return rc;
     const int64_t N = c->ncols - 1;
     std::vector<double> cr(N), cm(N, 0.0), row(c->ncols);
@@ -1647,6 +1750,7 @@ int lpg_solve_dual(lpg_ctx *c, int64_t max_pivots, lpg_result *out) {
     if (has_comm(c) && !(c->defer_k > 0 && c->nobj == 1))
         return fail(c, LPG_ERR_STATE, "lpg_solve_dual: a row partition runs the deferred form only (not LPG_FLAG_EAGER)");
     int rc;
+    if ((rc = usable(c))) return rc;
     if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;
     // the dual simplex starts from a dual-feasible basis: every d_j >= -eps
     std::vector<double> obj(c->ncols);

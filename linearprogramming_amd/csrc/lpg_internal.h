@@ -61,6 +61,9 @@ struct DevState {
 };
 constexpr int64_t kStallResidency = 4;
 constexpr int64_t kStallPending = 5;
+// rq of a pending slot no pivot of the current block has filled (k_swap_plan
+// refuses it: a local row is in [-1, nloc))
+constexpr int64_t kNoSlot = INT64_MIN;
 
 // Pending-pivot buffers of the deferred update (Defer::on == 0: eager mode).
 struct Defer {
@@ -98,6 +101,11 @@ struct Xch {
     int64_t offF, offC;           // byte offsets of xF and xC (xP at 0)
     int64_t offG;                 // byte offset of the residency census words {gcnt, gdec} (rank 0's are used)
 };
+
+// The census words use [offG, offG + 72); the buffer owner's identity (PCI
+// bus id, 48 bytes, then its process id) sits at offG + kXchIdOff, read by
+// every peer when the push is attached (lpg_ctx.hip push_shares_device).
+constexpr int kXchIdOff = 128, kXchIdBytes = 64;
 
 // Ratio-test candidate: lexicographic (theta, key); row < 0 = none.
 struct Cand {                 // 32 B
@@ -202,7 +210,7 @@ int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, in
 // the pivot-row rewrite and the pending-counter reset (the rewrite's
 // multipliers come from launch_swap_plan, launched before either part)
 int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which);
-// reset = false: the caller clears npend / fwork itself (launch_fill_cols with st)
+// reset = false: the caller ends the block itself (launch_fill_cols with st)
 int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, bool reset = true);
 // Item map of the banded block pass (k_flushw): column tile
 // fastest, `rows`-row strips; when the rows hold >= 8 strips the last two are
@@ -253,9 +261,11 @@ int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0:
 int launch_swap_plan(const Launch &L, const Geo &g, DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
                      int32_t *pairs, int plan, int kmax);   // reads D.pv (replicated pivot elements)
 int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs);
-// st != nullptr: also clears the pending block (npend, fwork), in place of
-// launch_flush_tail's memset (one dispatch fewer per block)
-int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs, DevState *st = nullptr);
+// st != nullptr: also ends the pending block (npend, fwork, and D's kmax slots
+// back to their never-filled sentinels), in place of launch_flush_tail's
+// k_end_block (one dispatch fewer per block)
+int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs, DevState *st = nullptr,
+                     const Defer *D = nullptr, int kmax = 0);
 // Canonical order again: rows [i0, i0 + nr) gathered through inv into tmp
 // (nr x ld), then copied back; launch_iota resets colmap / inv.
 int launch_gather_rows(const Launch &L, const Geo &g, const int32_t *inv, double *tmp, int64_t i0, int64_t nr);

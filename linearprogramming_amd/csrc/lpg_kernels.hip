@@ -2320,12 +2320,31 @@ __global__ __launch_bounds__(kBlock) void k_move_cols(double *__restrict__ T, Ge
 // grid: (row blocks, 4): constraint row i, pairs p = blockIdx.y (mod 4).
 // st: the pending block is applied, clear it and the dequeue head (no kernel
 // of this launch reads them)
-__global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Geo g, const int32_t *__restrict__ pairs,
-                                                      DevState *__restrict__ st) {
-    if (st && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+// End of a block, after every consumer of its slots (the plan, the pass, the
+// pivot-row rewrite): the slots return to the "never filled" sentinels, so a
+// later block whose npend runs ahead of the slots it filled (a block stopped
+// mid-way) meets a slot k_swap_plan refuses instead of the previous block's
+// in-range values: rq = kNoSlot (< -1), kq = lv = 0 (no column).
+__device__ __forceinline__ void end_block(DevState *st, const Defer &D, int kmax) {
+    const int q = threadIdx.x;
+    if (q == 0) {
         st->npend = 0;
         st->fwork = 0;
     }
+    for (int u = q; u < kmax; u += blockDim.x) {
+        D.rq[u] = kNoSlot;
+        if (D.kq) D.kq[u] = 0;
+        if (D.lv) D.lv[u] = 0;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_end_block(DevState *__restrict__ st, Defer D, int kmax) {
+    end_block(st, D, kmax);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Geo g, const int32_t *__restrict__ pairs,
+                                                      DevState *__restrict__ st, Defer D, int kmax) {
+    if (st && blockIdx.x == 0 && blockIdx.y == 0) end_block(st, D, kmax);
     const int n = pairs[0];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= g.nloc || n == 0) return;
@@ -2350,9 +2369,10 @@ int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const De
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs, DevState *st) {
+int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs, DevState *st, const Defer *D, int kmax) {
+    if (st && (!D || !D->rq || kmax < 1 || kmax > LPG_DEFER_MAX)) return -1;
     hipLaunchKernelGGL(k_fill_cols, dim3((unsigned)std::max<int64_t>((g.nloc + kBlock - 1) / kBlock, 1), 4), dim3(kBlock),
-                       0, (hipStream_t)L.stream, g.T, g, pairs, st);
+                       0, (hipStream_t)L.stream, g.T, g, pairs, st, D ? *D : Defer{}, kmax);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2413,8 +2433,9 @@ int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &
                            D.Pbuf, D.mul, D.rq);
     if (hipGetLastError() != hipSuccess) return -1;
     if (!reset) return 0;
-    // the pending block is applied: clear it and the dequeue head
-    return hipMemsetAsync(&st->npend, 0, sizeof(int64_t) + sizeof(unsigned long long), stream) == hipSuccess ? 0 : -1;
+    // the pending block is applied: clear it, the dequeue head and the slots
+    hipLaunchKernelGGL(k_end_block, dim3(1), dim3(kBlock), 0, stream, st, D, kmax);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int variant) {

@@ -72,8 +72,9 @@ def device_count() -> int:
 class Engine:
     """One rank's engine for an m x ncols (= N+1) tableau."""
 
-    def __init__(self, m: int, ncols: int, device: int = 0, world: int = 1, rank: int = 0, flags: int = 0):
-        self.lib = L.load()
+    def __init__(self, m: int, ncols: int, device: int = 0, world: int = 1, rank: int = 0, flags: int = 0,
+                 lib=None):
+        self.lib = lib if lib is not None else L.load()
         self._ctx = ctypes.c_void_p()
         rc = self.lib.lpg_create_dist(ctypes.byref(self._ctx), device, world, rank, m, ncols, flags)
         if rc != 0:

@@ -94,3 +94,17 @@ def test_no_store_data_hazard_in_the_device_code():
     assert os.path.exists(LIB), "build first: make (or __graft_entry__.build())"
     hits = store_hazard_scan.scan(LIB)
     assert not hits, hits[:5]
+
+
+def test_fault_hook_only_in_the_test_hook_build():
+    """LPG_TEST_PENDING_FAULT (which corrupts the device's pending
+    block on purpose) is compiled into linearprogramming_amd/liblpg_testhooks.so
+    only; the product library carries no trace of it, and the hook build
+    exports the same boundary."""
+    hooks = os.path.join(ROOT, "linearprogramming_amd", "liblpg_testhooks.so")
+    assert os.path.exists(LIB) and os.path.exists(hooks), "build first: make (or __graft_entry__.build())"
+    assert b"LPG_TEST_PENDING_FAULT" not in open(LIB, "rb").read()
+    assert b"LPG_TEST_PENDING_FAULT" in open(hooks, "rb").read()
+    lib = ctypes.CDLL(hooks, mode=ctypes.RTLD_LOCAL)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing

@@ -279,29 +279,57 @@ def test_pricing_key_ties(lpg, monkeypatch, wg, defer, m, n, seed):
 
 
 @pytest.mark.parametrize("persist", [None, 0])
-@pytest.mark.parametrize("what", ["npend", "kq", "lv", "rq"])
+@pytest.mark.parametrize("what", ["npend", "kq", "lv", "rq", "ahead"])
 def test_inconsistent_pending_block_stops_numeric(lpg, monkeypatch, what, persist):
     """k_swap_plan's guard (a stopped block left npend
     ahead of the slots it filled, and the plan indexed inv / colmap / Cbuf
-    with what it found, faulting the GPU). The test hook corrupts the pending
-    block before the second flush, with the column trade on: the loop stops
-    with NUMERIC, the flush applies nothing, lpg_last_error names the field --
-    and the GPU is healthy after it (a fresh engine solves bitwise)."""
+    with what it found, faulting the GPU). The test-hook build
+    (liblpg_testhooks.so; the product library has no hook) corrupts the
+    pending block before the second flush, with the column trade on: the loop
+    stops with NUMERIC, the flush applies nothing, lpg_last_error names the
+    field. "ahead" leaves npend one past the slots a partial block filled:
+    the slot it reaches holds the never-filled sentinels every block end
+    writes back, not the previous block's in-range values, so the
+    plan refuses it as well. The context then refuses every pivoting call
+    until the LP is regenerated (its basis and constraint rows
+    disagree), after which it solves bitwise -- and the GPU is healthy."""
+    from linearprogramming_amd import _lib as L
     m, n = 600, 1100
+    hooks = L.load_testhooks()
     monkeypatch.setenv("LPG_TEST_PENDING_FAULT", f"1:{what}")
     monkeypatch.setenv("LPG_NO_REORDER", "0")          # the column trade on: the plan indexes with kq / lv
-    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32, persist=persist)
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32, persist=persist, lib=hooks)
     monkeypatch.delenv("LPG_TEST_PENDING_FAULT")
     assert e.info.column_trade == 1 and (e.info.pivot_wg > 0) == (persist is None)
     e.generate(n, 5, 0)
-    with pytest.raises(lpg.LPGError, match=rf"pending block inconsistent at the flush \({what}\["):
+    # "ahead": 40 pivots = one full block, then a partial one of 8 (flush 1 at the solve's end)
+    field = "kq" if what == "ahead" else what
+    with pytest.raises(lpg.LPGError, match=rf"pending block inconsistent at the flush \({field}\["):
+        e.solve(40 if what == "ahead" else 100_000, 0)
+    with pytest.raises(lpg.LPGError, match=r"context unusable"):
         e.solve(100_000, 0)
-    e.close()
-    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32, persist=persist)
-    e.generate(n, 5, 0)
+    e.generate(n, 5, 0)                                # a rewritten tableau: usable again
     res = e.solve(100_000, 0)
     o = Oracle(m, n + m + 1)
     o.generate(n, 5, 0)
     ores = o.solve(100_000, 0)
     assert res.status == ores.status == 1 and res.pivots == ores.pivots > 64
     _assert_same(e, o, m)
+    e.close()
+
+
+def test_product_library_has_no_test_hook(lpg, monkeypatch):
+    """the fault hook is compiled into the test-hook build only --
+    the product library ignores LPG_TEST_PENDING_FAULT and solves bitwise."""
+    m, n = 600, 1100
+    monkeypatch.setenv("LPG_TEST_PENDING_FAULT", "1:npend")
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32)
+    monkeypatch.delenv("LPG_TEST_PENDING_FAULT")
+    e.generate(n, 5, 0)
+    res = e.solve(100_000, 0)
+    o = Oracle(m, n + m + 1)
+    o.generate(n, 5, 0)
+    ores = o.solve(100_000, 0)
+    assert res.status == ores.status == 1 and res.pivots == ores.pivots
+    _assert_same(e, o, m)
+    e.close()

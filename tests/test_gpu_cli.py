@@ -33,8 +33,10 @@ def _fnv(k, r):
 
 
 def _cli(args, env=None, timeout=120):
+    # `--gpus P` forks P ranks onto the test box's ONE GPU: acknowledge that for
+    # the owner push (refused at attach otherwise, lpg_ctx.hip push_shares_device)
     p = subprocess.run([CLI] + args, capture_output=True, text=True, timeout=timeout,
-                       env={**os.environ, **(env or {})})
+                       env={**os.environ, "LPG_PUSH_SHARED_DEVICE": "1", **(env or {})})
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     return p, lines
 

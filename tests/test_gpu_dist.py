@@ -113,6 +113,18 @@ def lpg():
     return lpg
 
 
+@pytest.fixture(autouse=True)
+def _acknowledge_shared_gpu(monkeypatch, request):
+    """Every multi-rank case here runs on the ONE GPU of the test box, so the
+    owner push would be refused at attach time (ranks sharing a process's
+    queues or a GPU's CUs, lpg_ctx.hip push_shares_device): these tests keep
+    exercising the protocol at sizes whose grids co-reside, and say so. The
+    refusals themselves are tested below with the acknowledgements cleared."""
+    if "refused" not in request.node.name:
+        monkeypatch.setenv("LPG_PUSH_SHARED_QUEUES", "1")
+        monkeypatch.setenv("LPG_PUSH_SHARED_DEVICE", "1")
+
+
 @pytest.mark.parametrize("defer", [None, "0", "5", "64", "128"])
 @pytest.mark.parametrize("world,m,n,kind,rule", [(2, 96, 160, 0, 0), (3, 101, 77, 0, 0), (2, 64, 64, 1, 1),
                                                  (4, 203, 301, 0, 0), (8, 203, 301, 0, 0)])
@@ -435,3 +447,49 @@ def test_bench_torchrun_4_ranks(world, exchange):
         assert d["config"]["pivot_loop"].startswith("k_pivot_block"), d["config"]
     assert d["config"]["pivots_timed"] > 0 and d["config"]["pivots_timed"] % 4 == 0
     assert "using the collectives" not in p.stderr
+
+
+def test_push_between_threads_refused(lpg, monkeypatch):
+    """ranks that are threads of one process share its
+    hardware queues, so a spinning exchange kernel can sit in front of the
+    peer kernel it waits for (tools/soak_dist.py's 2 s timeouts mid-solve).
+    lpg_comm_init_push_local refuses that at attach time with a named error,
+    before any pivot; the ranks keep their collectives."""
+    monkeypatch.delenv("LPG_PUSH_SHARED_QUEUES", raising=False)
+    es = [lpg.Engine(64, 64 + 128 + 1, world=2, rank=r) for r in range(2)]
+    for e in es:
+        e.comm_init_host(lambda b: b, lambda a: a)
+    bases = [e.push_base() for e in es]
+    for e in es:
+        with pytest.raises(lpg.LPGError, match=r"owner-push exchange refused: the 2 ranks are threads of one process"):
+            e.comm_init_push_local(bases)
+        assert e.info.exchange == 0
+        e.close()
+
+
+def test_push_on_one_gpu_refused_bench_falls_back(monkeypatch):
+    """two processes on ONE GPU (the same PCI bus id in
+    their exchange buffers) share its CUs, so lpg_comm_init_push refuses the
+    owner push at attach time ("ranks 0 and 1 share GPU ...") and bench.py
+    falls back to the collectives before its first pivot -- the line reports
+    the collectives and a normal run, not a mid-solve timeout."""
+    import json
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--config", "2", "--host-comm", "--exchange", "push", "--steps", "2", "--warmup", "1", "--no-cpu"]
+    env = {k: v for k, v in os.environ.items() if k not in ("LPG_PUSH_SHARED_DEVICE", "LPG_PUSH_SHARED_QUEUES")}
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "owner-push exchange refused: ranks" in p.stderr and "share GPU" in p.stderr, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert "owner push" not in d["config"]["parallelism"] and d["config"]["pivots_timed"] > 0, d["config"]

@@ -51,6 +51,16 @@ def lpg():
     return lpg
 
 
+@pytest.fixture(autouse=True)
+def _acknowledge_shared_gpu(monkeypatch):
+    """The ranks here are processes on the test box's ONE GPU: the owner push
+    refuses that at attach time unless acknowledged (lpg_ctx.hip
+    push_shares_device; the refusal is tested in test_gpu_dist.py). The
+    persistent grids cannot co-reside at these sizes, so the residency census
+    hands these cases to the two-kernel pair, as before."""
+    monkeypatch.setenv("LPG_PUSH_SHARED_DEVICE", "1")
+
+
 def _sample(m, world, rank, k, seed):
     """k sampled global rows of rank `rank`'s block (floor(m p / W) split)."""
     r0, r1 = m * rank // world, m * (rank + 1) // world

@@ -9,6 +9,8 @@
 * config 5 (two-phase, Bland, m = n = 8192, KM-style degenerate with
   equality rows): the whole solve to optimality, bitwise against the oracle
   (status, pivot count, objective, log, basis, sampled rows).
+* config 4's width (196,609 columns) at m = 2048: 308 pivots through the
+  two-kernel pair with 96- and 64-pivot blocks, bitwise against the oracle.
 * config 4 (65536 x 131072, 103 GB tableau, one GPU): 320 pivots (three
   whole 96-pivot blocks, then a partial one of 32); the oracle cannot hold it, so size-independent properties over the
   WHOLE tableau, read back in row chunks: every basic column is a unit vector
@@ -154,3 +156,49 @@ def test_config4_full_size_properties(lpg):
     assert abs(obj[0] - zs[-1]) <= 1e-9 * abs(zs[-1])
     # the entered columns are basic now: their reduced costs are exactly 0 in the device row
     assert np.all(obj[basis] == 0.0)
+
+
+@pytest.fixture(scope="module")
+def width_oracle():
+    """Config 4's width (N + 1 = 196,609 columns) at m = 2048: the oracle's 308
+    pivots (3.2 GB tableau), shared by the K = 96 and K = 64 runs below."""
+    m, n, piv = 2048, 194560, 308
+    o = _oracle(m, n + m + 1)
+    o.generate(n, SEED, 0)
+    ores = o.solve(piv, 0)
+    assert ores.pivots == piv
+    yield m, n, piv, o, ores
+    o.close()
+
+
+@pytest.mark.parametrize("defer", [96, 64])
+def test_config4_width_bitwise(lpg, width_oracle, defer, monkeypatch):
+    """config 4's exact pivot path -- the two-kernel pair
+    (k_prep_d / k_select_d: 196,609 columns do not fit the persistent kernel's
+    slices) with 96-pivot blocks (config 4 on one GPU) and 64-pivot blocks
+    (one rank of its 8-way split) -- against the oracle at config 4's width:
+    308 pivots = three whole 96-pivot blocks + 20 (four whole 64-pivot blocks +
+    52), bitwise: pivot log, basis, objective row, column 0, every pivot row
+    and 64 sampled rows."""
+    m, n, piv, o, ores = width_oracle
+    monkeypatch.setenv("LPG_DEFER", str(defer))
+    e = lpg.Engine(m, n + m + 1)
+    monkeypatch.delenv("LPG_DEFER")
+    assert e.info.defer_k == defer and e.info.pivot_wg == 0 and e.info.column_trade == 1
+    e.generate(n, SEED, lpg.GEN_DENSE)
+    e.reserve_log(piv + 8)
+    res = e.solve(piv, lpg.RULE_DANTZIG)
+    assert res.status_name == "ITER_LIMIT" and res.pivots == piv and res.objective == ores.objective
+    log = _log(e)
+    assert log == _log(o)
+    basis = e.get_basis()
+    assert np.array_equal(basis, o.get_basis())
+    assert np.array_equal(e.get_rows(m, 1), o.get_rows(m, 1)), "objective row"
+    rng = np.random.default_rng(11)
+    rows = sorted(set(rng.choice(m, 64, replace=False).tolist()) | {r for _, r in log} | {0, m - 1})
+    x0 = e.get_column0()
+    for i in rows:
+        ri = e.get_rows(i, 1)
+        assert np.array_equal(ri, o.get_rows(i, 1)), f"row {i}"
+        assert x0[i] == ri[0, 0]
+    e.close()

@@ -1,6 +1,6 @@
 """Phase timing of the persistent pivot kernel (k_pivot_block) on config 3.
 
-Needs tools/liblpg_phases.so (make phases). One launch of a whole block; for
+Needs tools/probe/liblpg_phases.so (make phases). One launch of a whole block; for
 every pivot t the s_memrealtime (10 ns) stamps of thread 0 of workgroups 0
 and nwg/2: loop top, ratio decision known, row loads in, pricing record
 published, pricing decision known, ratio record published.
@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import linearprogramming_amd as lpg  # noqa: E402
 
-lib = lpg.load(os.path.join(ROOT, "tools", os.environ.get("PHASES_LIB", "liblpg_phases.so")))
+lib = lpg.load(os.path.join(ROOT, "tools", "probe", os.environ.get("PHASES_LIB", "liblpg_phases.so")))
 lib.lpg_debug_block_phases.restype = ctypes.c_int
 lib.lpg_debug_block_phases.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 m, n = int(os.environ.get("M", 16384)), int(os.environ.get("N", 32768))

@@ -1,6 +1,6 @@
 """Phase timing of the deferred pivot kernels (k_prep_d, k_select_d) on config 3.
 
-Needs tools/liblpg_phases.so (liblpg built with -DLPG_PHASES). For each pivot
+Needs tools/probe/liblpg_phases.so (liblpg built with -DLPG_PHASES). For each pivot
 position q in a block: s_memrealtime (10 ns) stamps of block 0 at the phase
 boundaries, relative to the earliest block start; plus the latest stamp over
 all blocks (~ kernel end).
@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import linearprogramming_amd as lpg  # noqa: E402
 
-lib = lpg.load(os.path.join(ROOT, "tools", "liblpg_phases.so"))
+lib = lpg.load(os.path.join(ROOT, "tools", "probe", "liblpg_phases.so"))
 lib.lpg_debug_phases.restype = ctypes.c_int
 lib.lpg_debug_phases.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 m, n = int(os.environ.get("M", 16384)), int(os.environ.get("N", 32768))

@@ -73,7 +73,6 @@ def main():
     # dominant kernel: the deferred block pass if it ran (k_flushw for 64-pivot blocks), else the eager update
     fk = out.get("FETCH_SIZE", {})
     kern = "k_flushw" if "k_flushw" in fk else ("k_flushm" if "k_flushm" in fk else "k_update")
-    pending = int(os.environ.get("PENDING", "64"))
     # FETCH_SIZE correction: x2 for 16-B/lane streaming reads (guide); other widths
     # are calibrated with tools/hbm_calib3 (--fetch-factor F)
     ff = float(os.environ.get("FETCH_FACTOR", "2.0"))
@@ -89,12 +88,29 @@ def main():
         out[f"{kern}_write_bytes"] = w_kb * 1024
     with open(os.path.join(ROOT, "profiles", f"r{rnd:02d}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
-    if upd is not None:
+    # the stamp, shape and pending count of the build the passes measured: from
+    # the bench lines those passes printed (bench.py attaches the traffic only
+    # to a line with the same stamp, kernel, pending count and m / n)
+    lines = []
+    for d in (f"pmc_r{rnd:02d}_fetch", f"pmc_r{rnd:02d}_write"):
+        try:
+            with open(os.path.join(OUT, d + ".json")) as f:
+                lines += [json.loads(x) for x in f if x.strip().startswith("{")]
+        except OSError:
+            pass
+    stamps = {x["roofline"].get("source_stamp") for x in lines}
+    shapes = {(x["config"]["m"], x["config"]["n"], x["roofline"].get("pending_pivots_per_launch")) for x in lines}
+    if upd is not None and len(lines) == 2 and len(stamps) == 1 and len(shapes) == 1 and None not in stamps:
+        (m, n, pend), = shapes
         with open(os.path.join(ROOT, "profiles", f"pmc_config{cfg}.json"), "w") as f:
             json.dump({"hbm_bytes_per_launch": upd, "source": f"profiles/r{rnd:02d}_pmc.json",
-                       "kernel": kern, "pending_pivots": pending, "fetch_factor": ff,
+                       "kernel": kern, "pending_pivots": pend, "m": m, "n": n, "source_stamp": stamps.pop(),
+                       "fetch_factor": ff,
                        "how": "tools/gpu.sh pmc steps: separate rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes "
-                              "of bench.py (whole 64-pivot blocks, no warm-up), means over the block passes"}, f, indent=1)
+                              "of bench.py (whole blocks, no warm-up), means over the block passes"}, f, indent=1)
+    elif upd is not None:
+        print(f"not writing pmc_config{cfg}.json: the two passes' bench lines disagree or are missing "
+              f"(stamps {stamps}, shapes {shapes})", file=sys.stderr)
     print(json.dumps(out, indent=1))
 
 
