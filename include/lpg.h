@@ -125,7 +125,10 @@ typedef struct {
     int32_t residency_fallbacks;  /* persistent pivot launches that found their grid (every rank's) not resident
                                      at once -- another kernel or process held CUs -- and handed the loop to the
                                      two-kernel pair (pivot_wg is 0 from then on) */
-    int32_t pad0;
+    int32_t region;             /* 1: the persistent pivot kernel runs in region mode -- its slices hold only the
+                                   block start's nonbasic columns plus a spare slot per pending pivot for the
+                                   column leaving the basis then (one rank, one objective row, column trade on;
+                                   the default where it fits, env LPG_REGION=0 turns it off) */
 } lpg_info_t;
 
 typedef struct {

@@ -42,7 +42,7 @@ class Info(ctypes.Structure):
                 ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("nobj", ctypes.c_int32), ("defer_k", ctypes.c_int32), ("pivot_wg", ctypes.c_int32),
                 ("bytes_per_pivot", ctypes.c_double), ("exchange", ctypes.c_int32), ("column_trade", ctypes.c_int32),
-                ("residency_fallbacks", ctypes.c_int32), ("pad0", ctypes.c_int32)]
+                ("residency_fallbacks", ctypes.c_int32), ("region", ctypes.c_int32)]
 
 
 class Timing(ctypes.Structure):

@@ -425,14 +425,16 @@ __device__ __forceinline__ double chain_n(const double *own, const double *uni, 
     }
     return x;
 }
-template <bool ROW, bool SEL>
+template <bool ROW, bool SEL, bool B2>
 __device__ __forceinline__ double chain(const double *own, const double *uni, int nb, int lim, double x) {
-    switch (nb) {      // nb <= 4: blocks of <= 64 pivots (block_geometry)
+    switch (nb) {      // nb <= KB / 16: blocks of <= 64 or <= 96 pivots (block_geometry)
         case 0: return x;
         case 1: return chain_n<ROW, SEL, 1>(own, uni, lim, x);
         case 2: return chain_n<ROW, SEL, 2>(own, uni, lim, x);
         case 3: return chain_n<ROW, SEL, 3>(own, uni, lim, x);
-        default: return chain_n<ROW, SEL, 4>(own, uni, lim, x);
+        case 4: return chain_n<ROW, SEL, 4>(own, uni, lim, x);
+        case 5: return B2 ? chain_n<ROW, SEL, 5>(own, uni, lim, x) : x;
+        default: return B2 ? chain_n<ROW, SEL, 6>(own, uni, lim, x) : x;
     }
 }
 
@@ -454,6 +456,11 @@ struct BlockArgs {
     uint32_t tag0;               // tag of pivot i of this launch = tag0 + 1 + i (never repeats per context)
     int nwg, cw, rw, ks;         // workgroups, columns / rows per slice, LDS slots
     uint32_t cl;                 // residency census: this launch's index since the DevState was reset (1-based)
+    // REG (region mode): the slices hold the live columns only (below)
+    const int32_t *live;         // nlive physical columns, nonbasic at the block start, column 0 excluded
+    int64_t nlive;
+    const int64_t *bcol0;        // m: (logical << 32) | physical column of row r's basic variable at the block start
+    int nsp, cwx;                // spare column slots per workgroup; thread rows of the sP slice
 };
 
 // MR (multi-rank, row partition; Xch attached): the leaving row is the
@@ -464,8 +471,36 @@ struct BlockArgs {
 // exchange: P and the objective rows are replicated, so every rank takes the
 // same entering column from its own records. rq holds LOCAL rows (-1: another
 // rank's), the replicated basis / lv are kept by workgroup 0 of every rank.
-template <int RULE, int NOBJ, bool MR>
+// KB: the pending slots a block may hold, 64 or 96. Pending pivot u's per-slot
+// scalars (its row r_u, the multipliers -C_u[r], the entering column's P_u[k])
+// sit in lane u of every wave -- for KB = 96 a second bank of registers holds
+// slots 64..95 in lanes 0..31 (B2).
+//
+// REG (region mode, one objective row): the column slices hold only the
+// columns whose pending P entries can be nonzero. A column basic at the block
+// start has P_u = +0 at every pivot until it leaves the basis (its column is
+// the unit vector e_r, so the pivot row's entry is +0 unless the pivot row is
+// r), so the slices hold the nonbasic columns of the block start (a.live:
+// with the column trade these keep their physical positions from block to
+// block) and, per pending pivot sq, one spare slot (workgroup sq mod nwg,
+// thread cw + sq / nwg) that takes over the column leaving the basis at pivot
+// sq when row r_sq was not pivoted earlier in the block (otherwise the leaving
+// variable entered during the block and is a live column already). At its
+// leaving pivot the spare evaluates the chain from the base value 1.0 (row
+// r_sq of e_r) over its +0 slots -- the value every column thread of the
+// all-column form computes -- while it looks up the column (a.bcol0[r_sq]);
+// it stores that slot and applies its objective update at the next pivot, before
+// any reader (never priced at its own leaving pivot: d_L = -d_k P_q[L] >= 0,
+// so not eligible). Workgroup 0's thread cw + nsp holds column 0 (b).
+// Preconditions kept by the host (lpg_ctx.hip region_setup): basic columns
+// are exact unit vectors with zero reduced costs, every block's column trade
+// was complete (k_swap_plan sets DevState::rbad otherwise and the launch
+// stops with kStallRegion), end_block zeroes the spares' Pbuf columns.
+template <int RULE, int NOBJ, bool MR, int KB, bool REG>
 __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
+    static_assert(!REG || (NOBJ == 1 && !MR), "region mode: one objective row, one rank");
+    constexpr bool B2 = KB > 64;
+    constexpr int WS = B2 ? 104 : 72;                // per-wave slot rows of wm / wp
     // pricing record granules: {key, j} {P_q[phys], phys} [{dR}] [{dM}], and one
     // extra granule {P_q[0]} after the nwg records (workgroup 0's). Dantzig on
     // one objective row carries no dR: the key holds it (cls 0, ~bits(dR) in the
@@ -492,7 +527,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     // and the entering column's P_u[k] (phase S); slots 64..71 are the
     // padding a batch of 8 may reach: -0 and +0, so a padded step
     // fma(-0, +0, x) / fma(-(+0), +0, x) is exactly x
-    __shared__ __attribute__((aligned(16))) double wm[kNT / 64][72], wp[kNT / 64][72];
+    __shared__ __attribute__((aligned(16))) double wm[kNT / 64][WS], wp[kNT / 64][WS];
     const Geo &g = a.g;
     const Defer &D = a.D;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -502,13 +537,37 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     // 64 banks once). Slots past the pending block stay +0, so the chains'
     // padding steps (a batch of 8 past q) are exact no-ops.
     const int S = slot_stride(ks);
+    const int cwx = REG ? a.cwx : cw;                  // thread rows of sP (REG: + spares + column 0)
     double *sP = lds;
-    double *sC = lds + (size_t)S * cw;
-    double *sPt = sP + (size_t)(tid < cw ? tid : cw - 1) * S;   // this thread's slots (clamped: in bounds)
+    double *sC = lds + (size_t)S * cwx;
+    double *sPt = sP + (size_t)(tid < cwx ? tid : cwx - 1) * S;   // this thread's slots (clamped: in bounds)
     double *sCt = sC + (size_t)(tid < rw ? tid : rw - 1) * S;
     const int64_t ncp = (g.ncols + 1) & ~(int64_t)1;   // columns incl. the even padding one (k_flushw reads pairs)
-    const int64_t c = (int64_t)wg * cw + tid;          // this thread's physical column
-    const bool hc = tid < cw && c < ncp;
+    int64_t c = (int64_t)wg * cw + tid;                // this thread's physical column
+    bool hc = tid < cw && c < ncp;
+    int sq = -1;                                       // REG spare slot: the pending index it serves
+    if (REG) {
+        if (tid < cw) {
+            const int64_t k = (int64_t)wg * cw + tid;
+            hc = k < a.nlive;
+            c = hc ? a.live[k] : 0;
+        } else if (tid < cw + a.nsp) {
+            sq = wg + (tid - cw) * nwg;
+            if (sq >= ks) sq = -1;
+            hc = false;
+            c = 0;
+        } else {
+            hc = wg == 0 && tid == cw + a.nsp;         // column 0
+            c = 0;
+        }
+    }
+    const bool colwave = wave * 64 < cwx;              // this wave holds column threads (phase P's chain)
+    // REG spare state: at its leaving pivot (actq) the spare keeps P_actq there and
+    // that pivot's objective multiplier; its column ({logical, physical}) and the
+    // objective entry there land while the block goes on
+    int actq = -1;
+    double pql = 0.0, cobl = 0.0, dR0 = 0.0;
+    int64_t bc0 = 0;
     const int64_t i = (int64_t)wg * rw + tid;          // this thread's local constraint row
     const bool hr = tid < rw && i < g.nloc;
     const int64_t rM = g.nloc, rR = g.nloc + NOBJ - 1;
@@ -534,6 +593,18 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             return;
         }
     }
+    // ---- region mode: the live columns are the block start's nonbasic ones
+    // only while every block's column trade was complete (k_swap_plan clears
+    // nothing and sets rbad otherwise, e.g. after a forced pivot with a
+    // negative element); then no pivot runs and the host rebuilds the region
+    if (REG && st->rbad) {
+        if (wg == 0 && tid == 0) {
+            for (int u = 0; u < 2; u++)
+                if (st->slot[u].status == RUNNING) st->slot[u].status = ITER_LIMIT;
+            st->stall = kStallRegion;
+        }
+        return;
+    }
 
     // ---- launch start: everything here was written before the launch
     int s = a.s0;
@@ -543,14 +614,27 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     double cobjM = NOBJ == 2 ? a.Cs0[rM] : 0.0, cobjR = a.Cs0[rR];
     double dM = 0.0, dR = 0.0;
     int32_t lj = 0;
+    if (REG && sq >= 0 && sq < a.q0) {
+        // a spare of an earlier launch of this block: active iff the variable that
+        // left at pivot sq had not entered earlier in the block (then its row had
+        // not been pivoted); the earlier launch stored its slots and objective entry
+        const int64_t L = D.lv[sq];
+        bool fresh = L > 0;
+        for (int u = 0; u < sq; u++) fresh = fresh && D.kq[u] != L;
+        if (fresh) {
+            c = D.inv[L];
+            hc = true;
+        }
+    }
     if (hc) {
         if (NOBJ == 2) dM = g.T[rM * g.ld + c];
         dR = g.T[rR * g.ld + c];
         lj = D.colmap[c];
     }
     int64_t rqv = lane < a.q0 ? D.rq[lane] : -1;       // lane u: r_u of pending pivot u
+    int64_t rqv1 = B2 && 64 + lane < a.q0 ? D.rq[64 + lane] : -1;   // bank 1: r_{64 + lane}
     for (int u = 0; u < S; u++) {
-        if (tid < cw) sPt[u] = (u < a.q0 && hc) ? D.Pbuf[(int64_t)u * g.ld + c] : 0.0;
+        if (tid < cwx) sPt[u] = (u < a.q0 && hc) ? D.Pbuf[(int64_t)u * g.ld + c] : 0.0;
         if (tid < rw) sCt[u] = (u < a.q0 && hr) ? D.Cbuf[(int64_t)u * D.cs + i] : 0.0;
     }
     double b = 0.0;                                    // column 0 of the current tableau, this thread's row
@@ -565,17 +649,19 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     }
     {
         const double p0l = lane < a.q0 ? D.Pbuf[(int64_t)lane * g.ld] : 0.0;
-        const uint64_t p0b = (uint64_t)__double_as_longlong(p0l);
+        const double p0l1 = B2 && 64 + lane < a.q0 ? D.Pbuf[(int64_t)(64 + lane) * g.ld] : 0.0;
+        const uint64_t p0b = (uint64_t)__double_as_longlong(p0l), p0b1 = (uint64_t)__double_as_longlong(p0l1);
         for (int u = 0; u < a.q0; u++) {               // b = the pending chain over the earlier pivots
-            const double p0 = __longlong_as_double((long long)rdl64(p0b, u));
-            const int64_t ru = (int64_t)rdl64((uint64_t)rqv, u);
+            const bool hi = B2 && u >= 64;
+            const double p0 = __longlong_as_double((long long)(hi ? rdl64(p0b1, u - 64) : rdl64(p0b, u)));
+            const int64_t ru = (int64_t)(hi ? rdl64((uint64_t)rqv1, u - 64) : rdl64((uint64_t)rqv, u));
             if (hr) {
                 b = (i == ru) ? p0 : fma(-sCt[u], p0, b);
                 if (i == ru) lastpiv = u;
             }
         }
     }
-    if (lane < 8) {
+    if (lane < WS - 64) {
         wm[wave][64 + lane] = -0.0;
         wp[wave][64 + lane] = 0.0;
     }
@@ -663,8 +749,28 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         // this slice's base entries of row rs and the multipliers -C_u[rs]
         // (lane u < q; -0 past q): in flight across the barrier below
         const int64_t rloc = owns ? rs - g.row0 : -1;
-        const double xrow = (owns && hc) ? g.T[rloc * g.ld + c] : 0.0;
+        // REG: an active spare's first pivot after its leave (actq) completes it
+        // here, before the drain below: the leave's slot into Pbuf (a reader
+        // meets it at the earliest in this pivot's phase S, behind the pricing
+        // records) and its objective update; and the spare of this pivot takes
+        // the leaving column if row r was not pivoted earlier in the block
+        bool actnow = false;
+        if (REG) {
+            if (actq >= 0 && !hc) {
+                c = (int64_t)(uint32_t)bc0;
+                lj = (int32_t)(bc0 >> 32);
+                hc = true;
+                dR = fma(-cobl, pql, dR0);
+                st_wt(D.Pbuf + (int64_t)actq * g.ld + c, pql);
+            }
+            const unsigned long long h0 = __ballot(lane < q && rqv == rs);
+            const unsigned long long h1 = B2 ? __ballot(64 + lane < q && rqv1 == rs) : 0ull;
+            actnow = sq == q && owns && (h0 | h1) == 0ull;
+            if (actnow) bc0 = a.bcol0[rs];               // {logical, physical}: needed from the next pivot on
+        }
+        const double xrow = (owns && hc) ? g.T[rloc * g.ld + c] : (actnow ? 1.0 : 0.0);
         const double mrow = (owns && lane < q) ? -ld_wt(D.Cbuf + (int64_t)lane * D.cs + rloc) : -0.0;
+        const double mrow1 = (B2 && owns && 64 + lane < q) ? -ld_wt(D.Cbuf + (int64_t)(64 + lane) * D.cs + rloc) : -0.0;
         if (RPIV && pvneed) {
             // the winner's {piv, row} granule: stored with its {theta, row}, so
             // normally already visible; re-polled (bounded) if not
@@ -708,17 +814,19 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         // (the last pending pivot on rr), the base entries, the pending chain
         auto pivot_row = [&](bool on, int64_t rr) -> double {
             wm[wave][lane] = mrow;
+            if (B2 && lane < 32) wm[wave][64 + lane] = mrow1;
             const unsigned long long hit = __ballot(on && lane < q && rqv == rr);
-            const int qs = hit ? 63 - __clzll((long long)hit) : -1;
+            const unsigned long long hit1 = B2 ? __ballot(on && 64 + lane < q && rqv1 == rr) : 0ull;
+            const int qs = hit1 ? 127 - __clzll((long long)hit1) : (hit ? 63 - __clzll((long long)hit) : -1);
             double x = xrow;
             if (qs >= 0) x = sPt[qs];
             const double *wmw = &wm[wave][0];
-            if (!on) {
-                // another rank's row: its P slice arrives below
+            if (!on || !colwave) {
+                // another rank's row: its P slice arrives below (or no column in this wave)
             } else if (qs < 0) {
-                x = chain<true, false>(sPt, wmw, (q + 15) >> 4, qs, x);      // slots u < q
+                x = chain<true, false, B2>(sPt, wmw, (q + 15) >> 4, qs, x);      // slots u < q
             } else {
-                x = chain<true, true>(sPt, wmw, (q + 15) >> 4, qs, x);
+                x = chain<true, true, B2>(sPt, wmw, (q + 15) >> 4, qs, x);
             }
             return x;
         };
@@ -812,6 +920,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             lastpiv = q;
         }
         if (lane == q) rqv = rl;
+        if (B2 && 64 + lane == q) rqv1 = rl;
         LPG_BPH(t, 8);
         drain();                                        // the previous phase's C stores, before this record
         LPG_BPH(t, 9);
@@ -854,6 +963,12 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                 D.basis[r] = kt;
             }
         }
+        if (REG && actnow) {                           // the spare's slot q; Pbuf and d at the next pivot
+            pql = x / piv;
+            sPt[q] = pql;
+            cobl = cobjR;
+            actq = q;
+        }
         if (hc) {
             sPt[q] = pq;
             st_wt(D.Pbuf + (int64_t)q * g.ld + c, pq);  // drained in phase S, before the ratio record
@@ -879,9 +994,9 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                 rec_store(recP, wg * 16, pack(h, l, tag));
                 rec_store(recP, (nwg + wg) * 16, pack(0ull, ~0u, tag));
             }
-            // P_q[0] for every slice's column 0 (workgroup 0 holds column 0 in thread 0)
-            if (wg == 0) rec_store(recP, xidx * 16, pack((uint64_t)__double_as_longlong(pq), 0u, tag));
         }
+        // P_q[0] for every slice's column 0 (workgroup 0 holds column 0: thread 0, REG thread cw + nsp)
+        if (wg == 0 && hc && c == 0) rec_store(recP, xidx * 16, pack((uint64_t)__double_as_longlong(pq), 0u, tag));
         // the slice winner's objective entries and P_q entry ride along (C_{t+1}[obj]
         // and P_q[k] if it wins the grid); the thread of that column holds them
         if (PK1 && pb.j >= 0 && hc && (int64_t)lj == pb.j) {
@@ -1020,6 +1135,11 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         // u < q (Pbuf): in flight across the barrier below
         double xa = (okS > 0 && hr) ? g.T[i * g.ld + kp] : 0.0;
         double pu = (okS > 0 && wave * 64 < rw && lane < q) ? ld_wt(D.Pbuf + (int64_t)lane * g.ld + kp) : 0.0;
+        double pu1 = (B2 && okS > 0 && wave * 64 < rw && 64 + lane < q) ? ld_wt(D.Pbuf + (int64_t)(64 + lane) * g.ld + kp)
+                                                                         : 0.0;
+        // REG: the objective entry of the column that left at this pivot (as
+        // stored: a basic column's entry does not change while it stays basic)
+        if (REG && actq == q) dR0 = g.T[rR * g.ld + (int64_t)(uint32_t)bc0];
         if (PK1 && wave == 0 && g1src >= 0) {
             // the winner's {P_q[k], j}: stored with its key, so normally visible
             if (lane == 0) {
@@ -1064,6 +1184,8 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         // from the record; +0 past q)
         if (wave * 64 < rw)                             // waves holding rows
             wp[wave][lane] = lane == q ? pkq : pu;
+        if (B2 && wave * 64 < rw && lane < 32)
+            wp[wave][64 + lane] = 64 + lane == q ? pkq : pu1;
         LPG_BPH(t, 6);
         if (hr) b = (i == rl) ? p0q : fma(-sCt[q], p0q, b);
         // the chain over slots v <= q (q / 16 + 1 batches). A row pivoted earlier in this
@@ -1073,8 +1195,8 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         if (wave * 64 < rw) {                           // waves holding rows (xa is used under hr only)
             const double *wpw = &wp[wave][0];
             const bool sel = __ballot(hr && lastpiv >= 0) != 0ull;
-            if (!sel) xa = chain<false, false>(sCt, wpw, (q >> 4) + 1, lastpiv, xa);   // slots v <= q
-            else xa = chain<false, true>(sCt, wpw, (q >> 4) + 1, lastpiv, xa);
+            if (!sel) xa = chain<false, false, B2>(sCt, wpw, (q >> 4) + 1, lastpiv, xa);   // slots v <= q
+            else xa = chain<false, true, B2>(sCt, wpw, (q >> 4) + 1, lastpiv, xa);
         }
         LPG_BPH(t, 7);
         drain();                                        // this pivot's P stores, before the ratio record
@@ -1122,6 +1244,13 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         cobjM = nM;
         s = s1;
     }
+    // REG: a spare whose leave was the launch's last applied pivot completes it here
+    if (REG && actq >= 0 && !hc) {
+        c = (int64_t)(uint32_t)bc0;
+        hc = true;
+        dR = fma(-cobl, pql, g.T[rR * g.ld + c]);
+        D.Pbuf[(int64_t)actq * g.ld + c] = pql;
+    }
     // the objective row(s) of this slice, current after the last applied pivot
     if (hc) {
         if (NOBJ == 2) g.T[rM * g.ld + c] = dM;
@@ -1139,7 +1268,7 @@ int block_records_bytes(int nwg) { return nwg * (kRecPMax + kRecR) * 16; }
 // (config 2: 77.6k pivots/s on 256 workgroups, 99.8k on 16; config 5: 58.6k
 // on 256, 65.2k on 128; config 3 needs all 256 for the LDS).
 int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, int *rw, size_t *lds) {
-    if (ks < 1 || ks > 64) return -1;                      // blocks of <= 64 pivots (the slices' chains)
+    if (ks < 1 || ks > 96) return -1;                      // blocks of <= 96 pivots (the slices' chains, two lane banks)
     const int64_t ncp = (g.ncols + 1) & ~(int64_t)1;
     const int64_t S = slot_stride(ks);
     const int64_t per_wg = kMaxLds / (S * (int64_t)sizeof(double));   // columns + rows one workgroup holds
@@ -1165,13 +1294,114 @@ int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, i
     return 0;
 }
 
+// Region mode (REG, see k_pivot_block): the slices hold the nlive nonbasic
+// columns of the block start (column 0 excluded), nsp = ceil(ks / nwg) spare
+// slots per workgroup and column 0; the FEWEST workgroups whose slices fit
+// (threads cw + nsp + 1 <= 256 and rows <= 256, LDS within kMaxLds), then the
+// one-wave-of-rows rule of block_geometry.
+int block_geometry_region(const Geo &g, int ks, int cus, int want, int64_t nlive, RegionGeo *out) {
+    if (ks < 1 || ks > 96 || nlive < 1 || g.nobj != 1) return -1;
+    const int64_t S = slot_stride(ks);
+    const int64_t per_wg = kMaxLds / (S * (int64_t)sizeof(double));
+    auto fits = [&](int64_t w) {
+        const int64_t c = (nlive + w - 1) / w, r = (g.nloc + w - 1) / w, x = c + (ks + w - 1) / w + 1;
+        return w >= 1 && w <= kMaxWG && w <= cus && x <= kNT && r <= kNT && x + r <= per_wg;
+    };
+    int64_t w = want;
+    if (w <= 0) {
+        for (w = 1; w <= kMaxWG && w <= cus && !fits(w); w++) {
+        }
+        const int64_t w64 = (g.nloc + 63) / 64;
+        if (w >= 192 && w64 > w && fits(w64) && (g.nloc + w64 - 1) / w64 <= 64) w = w64;
+    }
+    if (!fits(w)) return -1;
+    out->nwg = (int)w;
+    out->cw = (int)((nlive + w - 1) / w);
+    out->rw = (int)((g.nloc + w - 1) / w);
+    out->nsp = (int)((ks + w - 1) / w);
+    out->cwx = out->cw + out->nsp + 1;
+    out->lds = (size_t)(S * (out->cwx + out->rw)) * sizeof(double);
+    return 0;
+}
+
+// ---- region-mode bookkeeping kernels (one workgroup each; bootstrap / rebuild only)
+
+// live: the physical columns in [1, ncols) holding no basic variable, ascending;
+// bcol0[r] = (basis[r] << 32) | its physical column; rbad cleared. mark: ld ints.
+__global__ __launch_bounds__(1024) void k_region_build(DevState *st, const int64_t *basis, const int32_t *inv,
+                                                        int64_t m, int64_t ncols, int32_t *mark, int32_t *live,
+                                                        int64_t *bcol0, int64_t nlive) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int64_t p = tid; p < ncols; p += nt) mark[p] = 0;
+    __syncthreads();
+    for (int64_t r = tid; r < m; r += nt) {
+        const int64_t v = basis[r];
+        const int32_t p = inv[v];
+        mark[p] = 1;
+        bcol0[r] = (v << 32) | (int64_t)(uint32_t)p;
+    }
+    __syncthreads();
+    // stable compaction of the unmarked columns 1..ncols-1: each thread a contiguous chunk
+    const int64_t per = (ncols - 1 + nt - 1) / nt, p0 = 1 + (int64_t)tid * per, p1 = std::min<int64_t>(p0 + per, ncols);
+    int cnt = 0;
+    for (int64_t p = p0; p < p1; p++) cnt += mark[p] == 0;
+    __shared__ int part[1024];
+    part[tid] = cnt;
+    __syncthreads();
+    for (int d = 1; d < nt; d <<= 1) {           // inclusive scan (Hillis-Steele)
+        const int v = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int64_t o = part[tid] - cnt;
+    for (int64_t p = p0; p < p1; p++)
+        if (mark[p] == 0 && o < nlive) live[o++] = (int32_t)p;
+    if (tid == 0) st->rbad = (part[nt - 1] == nlive) ? 0u : 2u;   // 2: the basis is not m distinct columns
+}
+
+// the region's preconditions on this tableau: every basic column an exact unit
+// vector (1.0 in its row, +-0 elsewhere) with a zero reduced cost; ok[0] = 0
+// on the first violation. Grid: (rows / 64, basic variables / 256).
+__global__ __launch_bounds__(256) void k_region_check(const double *T, Geo g, const int64_t *basis,
+                                                       const int32_t *inv, int *ok) {
+    const int64_t r = (int64_t)blockIdx.y * 256 + threadIdx.x;     // basic variable of row r
+    if (r >= g.m) return;
+    const int64_t p = inv[basis[r]];
+    bool good = true;
+    const int64_t i0 = (int64_t)blockIdx.x * 64, i1 = std::min<int64_t>(i0 + 64, g.nloc + g.nobj);
+    for (int64_t i = i0; i < i1; i++) {
+        const double v = T[i * g.ld + p];
+        good = good && (i < g.nloc ? v == (i == r ? 1.0 : 0.0) : v == 0.0);
+    }
+    if (!good) ok[0] = 0;
+}
+
+int launch_region_build(const Launch &L, const Geo &g, DevState *st, const int64_t *basis, const int32_t *inv,
+                        int32_t *mark, int32_t *live, int64_t *bcol0, int64_t nlive) {
+    hipLaunchKernelGGL(k_region_build, dim3(1), dim3(1024), 0, (hipStream_t)L.stream, st, basis, inv, g.m, g.ncols,
+                       mark, live, bcol0, nlive);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_region_check(const Launch &L, const Geo &g, const int64_t *basis, const int32_t *inv, int *ok) {
+    if (g.nloc != g.m) return -1;                    // one rank
+    const int64_t rows = g.nloc + g.nobj;
+    hipLaunchKernelGGL(k_region_check, dim3((unsigned)((rows + 63) / 64), (unsigned)((g.m + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)L.stream, g.T, g, basis, inv, ok);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, int s0, int q0, int n, Cand *part,
                        int ncand, const Cand *cin, int ncin, const double *Cs0, double *Cs1, const Defer &D,
                        void *rec, uint32_t tag0, int nwg, int cw, int rw, int ks, size_t lds, uint32_t cl,
-                       const Xch *X, uint32_t xtag0) {
-    if (n < 1 || q0 < 0 || q0 + n > ks || ks > 64 || nwg < 1 || nwg > kMaxWG || ncand < nwg || cl < 1) return -1;
+                       const Xch *X, uint32_t xtag0, const RegionArgs *R) {
+    if (n < 1 || q0 < 0 || q0 + n > ks || ks > 96 || nwg < 1 || nwg > kMaxWG || ncand < nwg || cl < 1) return -1;
     if (X && (X->world < 1 || X->world > 64 || X->nblk < nwg || X->nx < 1)) return -1;
-    if ((int64_t)nwg * cw < ((g.ncols + 1) & ~(int64_t)1) || (int64_t)nwg * rw < g.nloc) return -1;
+    if (!R && ((int64_t)nwg * cw < ((g.ncols + 1) & ~(int64_t)1) || (int64_t)nwg * rw < g.nloc)) return -1;
+    if (R && (X || g.nobj != 1 || (int64_t)nwg * cw < R->nlive || (int64_t)nwg * rw < g.nloc ||
+              (int64_t)nwg * R->nsp < ks || R->cwx != cw + R->nsp + 1 || R->cwx > kNT || !R->live || !R->bcol0))
+        return -1;
     if (g.nobj != 1 && g.nobj != 2) return -1;
     BlockArgs a;
     a.T = g.T;
@@ -1196,29 +1426,42 @@ int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, in
     a.rw = rw;
     a.ks = ks;
     a.cl = cl;
+    a.live = R ? R->live : nullptr;
+    a.nlive = R ? R->nlive : 0;
+    a.bcol0 = R ? R->bcol0 : nullptr;
+    a.nsp = R ? R->nsp : 0;
+    a.cwx = R ? R->cwx : cw;
     hipStream_t stream = (hipStream_t)L.stream;
     // the dynamic-LDS limit is a per-device attribute: set once per device
     // (bit `dev` of a per-kernel mask; ranks as threads may race to set it,
     // which is harmless)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
-#define LPG_PB(R, NO, M)                                                                                \
+#define LPG_PB(RU, NO, M, KB, RG)                                                                       \
     do {                                                                                                \
         static std::atomic<unsigned long long> attr{0};                                                 \
         if (!((attr.load(std::memory_order_acquire) >> dev) & 1ull)) {                                   \
-            if (hipFuncSetAttribute((const void *)k_pivot_block<R, NO, M>,                              \
+            if (hipFuncSetAttribute((const void *)k_pivot_block<RU, NO, M, KB, RG>,                     \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds) != hipSuccess) \
                 return -1;                                                                              \
             attr.fetch_or(1ull << dev, std::memory_order_acq_rel);                                      \
         }                                                                                               \
-        hipLaunchKernelGGL((k_pivot_block<R, NO, M>), dim3(nwg), dim3(kNT), lds, stream, a);           \
+        hipLaunchKernelGGL((k_pivot_block<RU, NO, M, KB, RG>), dim3(nwg), dim3(kNT), lds, stream, a);  \
     } while (0)
-#define LPG_PB_M(R, NO)              \
-    do {                             \
-        if (X) LPG_PB(R, NO, true);  \
-        else LPG_PB(R, NO, false);   \
+#define LPG_PB_K(RU, NO, M, RG)                 \
+    do {                                        \
+        if (ks > 64) LPG_PB(RU, NO, M, 96, RG); \
+        else LPG_PB(RU, NO, M, 64, RG);         \
     } while (0)
-    if (rule == RULE_BLAND) {
+#define LPG_PB_M(RU, NO)                      \
+    do {                                      \
+        if (X) LPG_PB_K(RU, NO, true, false); \
+        else LPG_PB_K(RU, NO, false, false);  \
+    } while (0)
+    if (R) {
+        if (rule == RULE_BLAND) LPG_PB_K(RULE_BLAND, 1, false, true);
+        else LPG_PB_K(RULE_DANTZIG, 1, false, true);
+    } else if (rule == RULE_BLAND) {
         if (g.nobj == 2) LPG_PB_M(RULE_BLAND, 2);
         else LPG_PB_M(RULE_BLAND, 1);
     } else {
@@ -1226,6 +1469,7 @@ int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, in
         else LPG_PB_M(RULE_DANTZIG, 1);
     }
 #undef LPG_PB_M
+#undef LPG_PB_K
 #undef LPG_PB
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

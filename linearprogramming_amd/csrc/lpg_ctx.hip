@@ -72,6 +72,18 @@ struct lpg_ctx {
     bool no_reorder = false;      // LPG_NO_REORDER=1: keep the caller's column order (no block-end column trade)
     int pb_nwg = 0, pb_cw = 0, pb_rw = 0;
     size_t pb_lds = 0;
+    // region mode of the single-rank persistent launch (lpg_block.hip REG): the
+    // slices hold the block start's nonbasic columns only; needs one objective
+    // row, the column trade, and basic columns that are exact unit vectors with
+    // zero reduced costs (units_known: true after lpg_generate, or once
+    // region_setup's check passed; the engine's own pivots keep it)
+    bool reg = false;             // the single-rank persistent launch runs in region mode
+    bool reg_valid = false;       // live / bcol0 describe the current column order and basis
+    bool units_known = false;
+    RegionGeo rg{};
+    int32_t *live = nullptr, *mark = nullptr;
+    int64_t *bcol0 = nullptr;
+    int *rok = nullptr;           // region_check's flag
     void *rec = nullptr;          // its records (zeroed once; tags never repeat within a context)
     uint32_t tag = 0;
     uint32_t pb_launch = 0;       // persistent launches since the DevState was reset (the census index)
@@ -381,7 +393,8 @@ static int flush_launch(lpg_ctx *c) {
         return fail(c, LPG_ERR_DEVICE, "flush launch failed");
     if (re) {   // k_fill_cols also clears the pending block
         const Defer D = defer_of(c, 0);
-        if (launch_fill_cols(lau(c), geo(c), c->pairs, c->st, &D, flush_kmax_supported(c->defer_k)))
+        if (launch_fill_cols(lau(c), geo(c), c->pairs, c->st, &D, flush_kmax_supported(c->defer_k),
+                             c->reg ? c->bcol0 : nullptr))
             return fail(c, LPG_ERR_DEVICE, "fill launch failed");
         c->permuted = true;
     }
@@ -399,6 +412,7 @@ static int materialize(lpg_ctx *c) {
 // the pivot loop itself: host reads and writes, generic kernels).
 static int canonicalize(lpg_ctx *c) {
     int rc = materialize(c);
+    c->reg_valid = false;      // region mode rebuilds its live columns for the order and basis of the next launch
     if (rc || !c->permuted) return rc;
     const int64_t rows = c->nloc + c->nobj;
     if (!c->tmp) {
@@ -446,9 +460,11 @@ static int clear_candidates(lpg_ctx *c) {
     return 0;
 }
 
+static int region_setup(lpg_ctx *c);
+
 static int bootstrap(lpg_ctx *c, int rule) {
     int rc = canonicalize(c);
-    if (rc || (rc = clear_candidates(c))) return rc;
+    if (rc || (rc = region_setup(c)) || (rc = clear_candidates(c))) return rc;
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
     const Geo g = geo(c);
     if (launch_price(lau(c), g, rule, 0, c->st, 0, c->P, c->C[0], c->pp, c->pc, c->npp))
@@ -468,7 +484,7 @@ static int bootstrap(lpg_ctx *c, int rule) {
 // admits only row r (either sign, |T[r][k]| > eps_piv).
 static int bootstrap_forced(lpg_ctx *c, int rule, int64_t k, int64_t r) {
     int rc = canonicalize(c);
-    if (rc || (rc = clear_candidates(c))) return rc;
+    if (rc || (rc = region_setup(c)) || (rc = clear_candidates(c))) return rc;
     HIPCHK(c, hipMemsetAsync(c->st->slot, 0, sizeof(c->st->slot), c->stream));
     if (launch_select(lau(c), geo(c), rule, true, c->st, 0, 0, c->P, c->C[1], c->C[0], c->pp, c->npp, c->basis,
                       c->part, c->nsel, k, r, c->pc, c->skip, defer_of(c, 0)))
@@ -492,11 +508,55 @@ static int enqueue_eager(lpg_ctx *c, int64_t npiv, int rule);
 // its own count and the bootstraps clear the rest (clear_candidates).
 static int cand_cap(const lpg_ctx *c) { return std::max(c->nsel, c->nsel_d); }
 
+// Region mode's precondition on a tableau the engine did not generate
+// (lpg_load_rows / lpg_set_basis): every basic column an exact unit vector
+// with a zero reduced cost. Checked once (synchronously) at the next
+// bootstrap; the engine's own pivots keep it (an entering column becomes
+// exactly e_r: P_q[E] = piv / piv = 1, every other row fma(-x, 1, x) = +0, its
+// reduced cost fma(-d, 1, d) = 0). Where it fails the context leaves region
+// mode for good: the all-column slices if they fit this block size, else the
+// two-kernel pair.
+static int region_setup(lpg_ctx *c) {
+    if (!c->reg || c->units_known) return 0;
+    HIPCHK(c, hipMemsetAsync(c->rok, 0xff, sizeof(int), c->stream));
+    if (launch_region_check(lau(c), geo(c), c->basis, c->inv, c->rok)) return fail(c, LPG_ERR_DEVICE, "region check failed");
+    int ok = 0;
+    HIPCHK(c, hipMemcpyAsync(&ok, c->rok, sizeof ok, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (ok) {
+        c->units_known = true;
+        return 0;
+    }
+    c->reg = false;
+    if (c->pmr && !has_comm(c)) {
+        c->nsel_d = c->pb_nwg;
+    } else {
+        c->persist = false;
+        c->nsel_d = pivot_d_blocks(geo(c), 1, c->pivot_nt);   // <= the allocation
+    }
+    return 0;
+}
+
+// live columns and block-start basic columns for the current order and basis
+// (one workgroup, on the stream: no host sync); also clears DevState::rbad
+static int region_build(lpg_ctx *c) {
+    if (launch_region_build(lau(c), geo(c), c->st, c->basis, c->inv, c->mark, c->live, c->bcol0, c->ncols - 1 - c->m))
+        return fail(c, LPG_ERR_DEVICE, "region build failed");
+    c->reg_valid = true;
+    return 0;
+}
+
 // Persistent path: one k_pivot_block launch per run of pivots inside a
 // block, the block's flush after its last pivot.
 static int enqueue_blocks(lpg_ctx *c, int64_t npiv, int rule) {
     const Geo g = geo(c);
     const bool mr = c->persist_x && c->xmode;
+    const bool reg = c->reg && !mr && !has_comm(c);
+    if (reg && !c->reg_valid) {
+        int rc = region_build(c);
+        if (rc) return rc;
+    }
+    RegionArgs R{c->live, c->ncols - 1 - c->m, c->bcol0, c->rg.nsp, c->rg.cwx};
     while (npiv > 0) {
         const int n = (int)std::min<int64_t>(npiv, c->defer_k - c->pend);
         const int s0 = c->par, s1 = (s0 + n) & 1;
@@ -521,9 +581,15 @@ static int enqueue_blocks(lpg_ctx *c, int64_t npiv, int rule) {
             X.offC = c->xoffC;
             X.offG = c->xoffG;
         }
-        if (launch_pivot_block(lau(c), g, rule, c->st, s0, c->pend, n, c->part, ncand, cin, ncin, c->C[s0], c->C[s1],
-                               defer_of(c, c->pend), c->rec, c->tag, c->pb_nwg, c->pb_cw, c->pb_rw, c->defer_k,
-                               c->pb_lds, c->pb_launch + 1, mr ? &X : nullptr, c->xtag))
+        const bool ok = reg ? launch_pivot_block(lau(c), g, rule, c->st, s0, c->pend, n, c->part, ncand, cin, ncin,
+                                                 c->C[s0], c->C[s1], defer_of(c, c->pend), c->rec, c->tag, c->rg.nwg,
+                                                 c->rg.cw, c->rg.rw, c->defer_k, c->rg.lds, c->pb_launch + 1, nullptr,
+                                                 0, &R) == 0
+                            : launch_pivot_block(lau(c), g, rule, c->st, s0, c->pend, n, c->part, ncand, cin, ncin,
+                                                 c->C[s0], c->C[s1], defer_of(c, c->pend), c->rec, c->tag, c->pb_nwg,
+                                                 c->pb_cw, c->pb_rw, c->defer_k, c->pb_lds, c->pb_launch + 1,
+                                                 mr ? &X : nullptr, c->xtag) == 0;
+        if (!ok)
             return fail(c, LPG_ERR_DEVICE, "pivot block launch failed");
         c->pb_launch++;
         if (mr) {
@@ -743,6 +809,21 @@ static int recover_residency(lpg_ctx *c, const DevState &h) {
     return 0;
 }
 
+// A region-mode launch found DevState::rbad set (a block's column trade was
+// incomplete, so the block start's nonbasic columns moved) and ran no pivot,
+// nor did any launch after it: the next enqueue bootstraps (restoring the
+// caller's column order, then rebuilding the region, which clears rbad) and
+// lpg_sync re-runs the lost pivots, as after a residency abort.
+static int recover_region(lpg_ctx *c, const DevState &h) {
+    c->lost += std::max<int64_t>(c->enq - h.pivots, 0);
+    c->enq = h.pivots;
+    c->pend = (int)h.npend;
+    c->booted = false;
+    c->reg_valid = false;
+    HIPCHK(c, hipMemsetAsync(&c->st->stall, 0, sizeof(int64_t), c->stream));
+    return 0;
+}
+
 // k_swap_plan refused the pending block (lpg_kernels.hip): the loop was
 // stopped with NUMERIC and nothing of the block was applied.
 static int pending_fault(lpg_ctx *c, const DevState &h) {
@@ -773,6 +854,11 @@ static int read_result(lpg_ctx *c, lpg_result *out, int rule) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (h.stall == kStallResidency) {
         int rc = recover_residency(c, h);
+        if (rc) return rc;
+        h.stall = 0;
+    }
+    if (h.stall == kStallRegion) {
+        int rc = recover_region(c, h);
         if (rc) return rc;
         h.stall = 0;
     }
@@ -903,14 +989,6 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     // below 64-pivot passes), and the pair's chains are shorter at 96 --
     // config 4: 2,424 vs 2,347 pivots/s (profiles/r03_bench_config4_k96.json)
     const double tbytes = (double)nloc_guess * (double)ncols * 8.0;
-    const int kdef = tbytes >= 16e9 ? kDefaultDeferHuge : tbytes >= 200e6 ? kDefaultDefer : kDefaultDeferSmall;
-    c->defer_k = (flags & LPG_FLAG_EAGER) ? 0 : (dk ? atoi(dk) : kdef);
-    if (c->defer_k < 0 || c->defer_k > LPG_DEFER_MAX || (c->defer_k && !flush_kmax_supported(c->defer_k))) {
-        fail(c, LPG_ERR_ARG, "LPG_DEFER=%d out of range [0, %d]", c->defer_k, LPG_DEFER_MAX);
-        snprintf(g_err, sizeof g_err, "%s", c->err);
-        delete c;
-        return LPG_ERR_ARG;
-    }
     // the block-end column trade (§3.3 of DESIGN.md) pays where the block pass
     // is long; below 2 GB on one rank its kernels cost more than scattered
     // live columns do (config 2: 105k -> 112k pivots/s without it, config 5:
@@ -919,6 +997,37 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     c->no_reorder = nr ? atoi(nr) != 0 : (world == 1 && tbytes < 2e9);
     const char *sp = getenv("LPG_SLOW_PIVOT");
     c->fast_pivot = !(sp && atoi(sp));
+    // the persistent pivot launch (LPG_PERSIST=0: the two-kernel pair) and its
+    // region mode (one rank, one objective row, the column trade on;
+    // LPG_REGION=0: the all-column slices)
+    const char *pe = getenv("LPG_PERSIST"), *pw = getenv("LPG_PERSIST_WG"), *pr = getenv("LPG_REGION");
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
+    const bool persist_ok = c->fast_pivot && !(pe && atoi(pe) == 0) && cus > 0;
+    const bool reg_ok = persist_ok && world == 1 && c->nobj == 1 && !c->no_reorder && !(pr && atoi(pr) == 0);
+    const int64_t nlive = ncols - 1 - m;                 // nonbasic columns other than column 0 (any basis)
+    Geo g0{};
+    g0.nloc = nloc_guess;
+    g0.nobj = c->nobj;
+    g0.ncols = ncols;
+    g0.m = m;
+    int kdef = tbytes >= 16e9 ? kDefaultDeferHuge : tbytes >= 200e6 ? kDefaultDefer : kDefaultDeferSmall;
+    // region mode at 96-pivot blocks where the pass dominates (>= 2 GB) and the
+    // region's slices hold 96 slots: the 96-pivot pass costs ~12% less per
+    // pivot than the 64-pivot one (config-3 shape: 2.15 vs 1.625 ms per pass,
+    // profiles/r04_flush96_lab.log, r04_ab_k72_*), which the all-column
+    // slices could not hold (config 3: 49,153 columns at 96 slots = 37 MB of LDS)
+    RegionGeo rg96{};
+    if (reg_ok && tbytes >= 2e9 && tbytes < 16e9 && nlive > 0 &&
+        block_geometry_region(g0, 96, cus, pw ? atoi(pw) : 0, nlive, &rg96) == 0)
+        kdef = 96;
+    c->defer_k = (flags & LPG_FLAG_EAGER) ? 0 : (dk ? atoi(dk) : kdef);
+    if (c->defer_k < 0 || c->defer_k > LPG_DEFER_MAX || (c->defer_k && !flush_kmax_supported(c->defer_k))) {
+        fail(c, LPG_ERR_ARG, "LPG_DEFER=%d out of range [0, %d]", c->defer_k, LPG_DEFER_MAX);
+        snprintf(g_err, sizeof g_err, "%s", c->err);
+        delete c;
+        return LPG_ERR_ARG;
+    }
 #ifdef LPG_TEST_HOOKS
     // the test-hook build only (linearprogramming_amd/liblpg_testhooks.so,
     // Makefile): the product library never reads this variable
@@ -950,18 +1059,22 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         // the split is computed for the largest row block, so every rank of a
         // row partition gets the same workgroups, columns and rows per slice
         // (the multi-rank form exchanges P slice by slice)
-        const char *pe = getenv("LPG_PERSIST"), *pw = getenv("LPG_PERSIST_WG");
-        int cus = 0;
         Geo gm = g;
         gm.nloc = (m + world - 1) / world;
-        if (c->defer_k > 0 && c->fast_pivot && !(pe && atoi(pe) == 0) &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        if (c->defer_k > 0 && persist_ok &&
             block_geometry(gm, c->defer_k, cus, pw ? atoi(pw) : 0, &c->pb_nwg, &c->pb_cw, &c->pb_rw, &c->pb_lds) == 0) {
             c->pmr = true;
             if (world == 1) {
                 c->persist = true;
                 c->nsel_d = c->pb_nwg;      // one ratio candidate per workgroup
             }
+        }
+        // one rank: region mode where its slices fit (preferred over the all-column form)
+        if (c->defer_k > 0 && reg_ok && nlive > 0 &&
+            block_geometry_region(g, c->defer_k, cus, pw ? atoi(pw) : 0, nlive, &c->rg) == 0) {
+            c->reg = true;
+            c->persist = true;
+            c->nsel_d = c->rg.nwg;
         }
     }
 #define ALLOC(p, bytes)                                                                    \
@@ -983,8 +1096,15 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     ALLOC(c->cost, (size_t)ncols * sizeof(double));
     ALLOC(c->pp, (size_t)std::max(c->npp, c->npp_d) * sizeof(PricePart));
     ALLOC(c->pc, (size_t)c->npp * sizeof(int));
-    ALLOC(c->part, (size_t)std::max({c->nsel, c->nsel_d, c->pmr ? c->pb_nwg : 0}) * sizeof(Cand));
-    if (c->pmr) ALLOC(c->rec, (size_t)block_records_bytes(c->pb_nwg));
+    const int nwg_rec = std::max(c->pmr ? c->pb_nwg : 0, c->reg ? c->rg.nwg : 0);
+    ALLOC(c->part, (size_t)std::max({c->nsel, c->nsel_d, nwg_rec}) * sizeof(Cand));
+    if (nwg_rec) ALLOC(c->rec, (size_t)block_records_bytes(nwg_rec));
+    if (c->reg) {
+        ALLOC(c->live, (size_t)ncols * sizeof(int32_t));
+        ALLOC(c->mark, (size_t)c->ld * sizeof(int32_t));
+        ALLOC(c->bcol0, (size_t)m * sizeof(int64_t));
+        ALLOC(c->rok, sizeof(int));
+    }
     if (world > 1) ALLOC(c->cand, (size_t)std::max(c->nsel, c->nsel_d) * world * sizeof(Cand));
     else c->cand = c->part;
     ALLOC(c->basis, (size_t)m * sizeof(int64_t));
@@ -1026,7 +1146,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         (c->lv && hipMemset(c->lv, 0, (size_t)flush_kmax_supported(c->defer_k) * sizeof(int64_t)) != hipSuccess) ||
         (c->rq && hipMemset(c->rq, 0x80, (size_t)flush_kmax_supported(c->defer_k) * sizeof(int64_t)) != hipSuccess) ||
         (c->pv && hipMemset(c->pv, 0, (size_t)flush_kmax_supported(c->defer_k) * sizeof(double)) != hipSuccess) ||
-        (c->rec && hipMemset(c->rec, 0, (size_t)block_records_bytes(c->pb_nwg)) != hipSuccess) ||
+        (c->rec && hipMemset(c->rec, 0, (size_t)block_records_bytes(nwg_rec)) != hipSuccess) ||
         (c->colmap && (launch_iota(lau(c), c->colmap, c->ld) || launch_iota(lau(c), c->inv, c->ld)))) {
         fail(c, LPG_ERR_DEVICE, "hipMemset failed");
         lpg_destroy(c);
@@ -1256,7 +1376,7 @@ void lpg_destroy(lpg_ctx *c) {
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
                     c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->mul, c->pv, c->tmp,
-                    c->rec, c->drc, c->dcp, c->drc_all};
+                    c->rec, c->drc, c->dcp, c->drc_all, c->live, c->mark, c->bcol0, c->rok};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -1275,12 +1395,12 @@ int lpg_info(const lpg_ctx *c, lpg_info_t *o) {
     o->device = c->device;
     o->nobj = (int32_t)c->nobj;
     o->defer_k = c->defer_k;
-    o->pivot_wg = ((c->persist && !has_comm(c)) || (c->persist_x && c->xmode)) ? c->pb_nwg : 0;
+    o->pivot_wg = (c->persist && !has_comm(c)) ? (c->reg ? c->rg.nwg : c->pb_nwg) : ((c->persist_x && c->xmode) ? c->pb_nwg : 0);
     o->bytes_per_pivot = 16.0 * (double)(c->nloc + c->nobj) * (double)c->ncols;
     o->exchange = c->xmode ? (c->xuncached ? 2 : 1) : 0;
     o->column_trade = reorders(c) ? 1 : 0;
     o->residency_fallbacks = c->res_fallbacks;
-    o->pad0 = 0;
+    o->region = (o->pivot_wg > 0 && c->reg && !has_comm(c)) ? 1 : 0;
     return 0;
 }
 
@@ -1305,6 +1425,7 @@ int lpg_load_rows(lpg_ctx *c, int64_t row0, int64_t nrows, const double *rows, i
                                 hipMemcpyHostToDevice));
     }
     c->poisoned = false;   // the caller rewrites the tableau (its pending block was cleared at the refusal)
+    c->units_known = false;   // region mode checks the basic columns first (region_setup)
     return reset_state(c);
 }
 
@@ -1316,6 +1437,7 @@ int lpg_set_basis(lpg_ctx *c, const int64_t *basis) {
     if ((rc = use_device(c)) || (rc = canonicalize(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(c->basis, basis, c->m * sizeof(int64_t), hipMemcpyHostToDevice));
+    c->units_known = false;
     return reset_state(c);
 }
 
@@ -1394,6 +1516,7 @@ int lpg_generate(lpg_ctx *c, int64_t n, uint64_t seed, int kind) {
     c->pend = 0;                 // the generator overwrites the whole tableau: nothing pending survives
     if (launch_generate(lau(c), geo(c), n, seed, kind, c->basis)) return fail(c, LPG_ERR_DEVICE, "generate launch failed");
     c->poisoned = false;   // the whole tableau and the basis are rewritten
+    c->units_known = true; // the generator writes exact unit columns for the slack / artificial basis
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return reset_state(c);
 }

@@ -58,9 +58,13 @@ struct DevState {
     int64_t stall_info[4];        // its view then: phase (1 P, 2 S), expected tag, record index, tag seen
     uint32_t rcnt;                // k_pivot_block residency census: arrivals (launch L's count from L * nwg)
     uint32_t rdec;                // its decision word: (L << 2) | kGo / kAbort (single rank)
+    uint32_t rbad;                // region mode invalid: 1 a block's column trade was incomplete (k_swap_plan),
+                                  // 2 the region build found no m distinct basic columns; 0 once rebuilt
+    uint32_t pad1;
 };
 constexpr int64_t kStallResidency = 4;
 constexpr int64_t kStallPending = 5;
+constexpr int64_t kStallRegion = 6;   // a region-mode launch found rbad set and ran no pivot
 // rq of a pending slot no pivot of the current block has filled (k_swap_plan
 // refuses it: a local row is in [-1, nloc))
 constexpr int64_t kNoSlot = INT64_MIN;
@@ -200,10 +204,32 @@ int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, i
 // exchange words): if the whole grid is not resident within a bound, the
 // launch does nothing, stops the loop (both slots non-RUNNING) and sets
 // DevState::stall = kStallResidency; the host then continues on the pair.
+// Region mode (single rank, one objective row, column trade on): the slices
+// hold only the columns whose pending P entries can be nonzero -- the nonbasic
+// columns of the block start (live, column 0 excluded) plus per pending pivot
+// one spare slot for the column leaving the basis then, and column 0 (lpg_block.hip
+// k_pivot_block). block_geometry_region picks the split; launch_region_build
+// (one workgroup) writes live and bcol0 from the basis and clears rbad;
+// launch_region_check clears ok[0] unless every basic column is an exact unit
+// vector with a zero reduced cost (the region's precondition).
+struct RegionGeo {
+    int nwg, cw, rw, nsp, cwx;
+    size_t lds;
+};
+struct RegionArgs {
+    const int32_t *live;
+    int64_t nlive;
+    const int64_t *bcol0;
+    int nsp, cwx;
+};
+int block_geometry_region(const Geo &g, int ks, int cus, int want, int64_t nlive, RegionGeo *out);
+int launch_region_build(const Launch &L, const Geo &g, DevState *st, const int64_t *basis, const int32_t *inv,
+                        int32_t *mark, int32_t *live, int64_t *bcol0, int64_t nlive);
+int launch_region_check(const Launch &L, const Geo &g, const int64_t *basis, const int32_t *inv, int *ok);
 int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, int s0, int q0, int n, Cand *part,
                        int ncand, const Cand *cin, int ncin, const double *Cs0, double *Cs1, const Defer &D,
                        void *rec, uint32_t tag0, int nwg, int cw, int rw, int ks, size_t lds, uint32_t cl,
-                       const Xch *X = nullptr, uint32_t xtag0 = 0);
+                       const Xch *X = nullptr, uint32_t xtag0 = 0, const RegionArgs *R = nullptr);
 // Apply the pending pivots (st->npend <= kmax) to constraint rows 0..nloc-1.
 int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which);
 // ... in two parts: the block pass itself (k_flushw / k_flushm / k_flush), then
@@ -264,8 +290,10 @@ int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const De
 // st != nullptr: also ends the pending block (npend, fwork, and D's kmax slots
 // back to their never-filled sentinels), in place of launch_flush_tail's
 // k_end_block (one dispatch fewer per block)
+// bcol0 != nullptr (region mode, one rank): also the spares' Pbuf columns
+// zeroed and every row's basic column of the next block written
 int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs, DevState *st = nullptr,
-                     const Defer *D = nullptr, int kmax = 0);
+                     const Defer *D = nullptr, int kmax = 0, int64_t *bcol0 = nullptr);
 // Canonical order again: rows [i0, i0 + nr) gathered through inv into tmp
 // (nr x ld), then copied back; launch_iota resets colmap / inv.
 int launch_gather_rows(const Launch &L, const Geo &g, const int32_t *inv, double *tmp, int64_t i0, int64_t nr);

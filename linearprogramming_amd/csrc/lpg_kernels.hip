@@ -2217,6 +2217,8 @@ __global__ __launch_bounds__(kPlanNT) void k_swap_plan(DevState *__restrict__ st
     int fx = q, fy = q;           // first event index of x / y, and its kind
     bool fxe = true, fye = false;
     const bool allpos = __syncthreads_count(!pos) == 0;   // also publishes sx / sy
+    // an incomplete trade moves the nonbasic columns: region mode must rebuild (DevState::rbad)
+    if (q == 0 && np > 0 && !allpos) st->rbad = 1;
 #pragma unroll 8
     for (int u = 0; u < np; u++) {
         const int64_t a = sx[u], b = sy[u];
@@ -2325,8 +2327,23 @@ __global__ __launch_bounds__(kBlock) void k_move_cols(double *__restrict__ T, Ge
 // later block whose npend runs ahead of the slots it filled (a block stopped
 // mid-way) meets a slot k_swap_plan refuses instead of the previous block's
 // in-range values: rq = kNoSlot (< -1), kq = lv = 0 (no column).
-__device__ __forceinline__ void end_block(DevState *st, const Defer &D, int kmax) {
+// Region mode (spare_zero, lpg_block.hip REG): a column that left the basis
+// during the block is held by a spare slot, which wrote its Pbuf entries; a
+// column that left and entered again stays basic and is held by nobody in the
+// next block, so its entries are zeroed here (every leaving column's, at its
+// position after the trade -- a live column's are rewritten by the next block
+// before they are read), keeping the next block's pass from applying them.
+__device__ __forceinline__ void end_block(DevState *st, const Defer &D, int kmax, bool spare_zero = false,
+                                          int64_t ld = 0) {
     const int q = threadIdx.x;
+    if (spare_zero) {
+        for (int e = q; e < kmax * kmax; e += blockDim.x) {
+            const int qq = e / kmax, u = e - qq * kmax;
+            const int64_t L = D.lv[qq];
+            if (L > 0) D.Pbuf[(int64_t)u * ld + D.inv[L]] = 0.0;
+        }
+        __syncthreads();
+    }
     if (q == 0) {
         st->npend = 0;
         st->fwork = 0;
@@ -2342,9 +2359,18 @@ __global__ __launch_bounds__(kBlock) void k_end_block(DevState *__restrict__ st,
     end_block(st, D, kmax);
 }
 
+// bcol0 (region mode): every row's basic column for the next block, {logical, physical}
 __global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Geo g, const int32_t *__restrict__ pairs,
-                                                      DevState *__restrict__ st, Defer D, int kmax) {
-    if (st && blockIdx.x == 0 && blockIdx.y == 0) end_block(st, D, kmax);
+                                                      DevState *__restrict__ st, Defer D, int kmax,
+                                                      int64_t *__restrict__ bcol0) {
+    if (st && blockIdx.x == 0 && blockIdx.y == 0) end_block(st, D, kmax, bcol0 != nullptr, g.ld);
+    if (bcol0 && blockIdx.y == 0) {
+        const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+        if (r < g.m) {
+            const int64_t v = D.basis[r];
+            bcol0[r] = (v << 32) | (int64_t)(uint32_t)D.inv[v];
+        }
+    }
     const int n = pairs[0];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= g.nloc || n == 0) return;
@@ -2369,10 +2395,12 @@ int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const De
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs, DevState *st, const Defer *D, int kmax) {
+int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs, DevState *st, const Defer *D, int kmax,
+                     int64_t *bcol0) {
     if (st && (!D || !D->rq || kmax < 1 || kmax > LPG_DEFER_MAX)) return -1;
+    if (bcol0 && (!st || g.nloc != g.m || !D->basis || !D->inv || !D->lv || !D->Pbuf)) return -1;   // region: one rank
     hipLaunchKernelGGL(k_fill_cols, dim3((unsigned)std::max<int64_t>((g.nloc + kBlock - 1) / kBlock, 1), 4), dim3(kBlock),
-                       0, (hipStream_t)L.stream, g.T, g, pairs, st, D ? *D : Defer{}, kmax);
+                       0, (hipStream_t)L.stream, g.T, g, pairs, st, D ? *D : Defer{}, kmax, bcol0);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

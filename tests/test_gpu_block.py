@@ -68,14 +68,15 @@ def test_engaged_where_the_slices_fit(lpg, monkeypatch):
     assert e.info.pivot_wg > 0
     assert _engine(lpg, monkeypatch, 600, 1701, defer=32, persist=0).info.pivot_wg == 0
     assert _engine(lpg, monkeypatch, 600, 1701, defer=0).info.pivot_wg == 0      # eager updates
-    assert _engine(lpg, monkeypatch, 600, 1701, defer=65).info.pivot_wg == 0     # blocks of > 64 pivots: the pair
+    assert _engine(lpg, monkeypatch, 600, 1701, defer=65).info.pivot_wg > 0      # 65..96: two lane banks
+    assert _engine(lpg, monkeypatch, 600, 1701, defer=97).info.pivot_wg == 0     # blocks of > 96 pivots: the pair
     # 256 workgroups hold at most 256 columns each: wider tableaus keep the pair
     assert _engine(lpg, monkeypatch, 8, 256 * 256 + 3, defer=8).info.pivot_wg == 0
 
 
 @pytest.mark.parametrize("trade", ["0", "1"])
 @pytest.mark.parametrize("wg", [None, 3, 7, 64, 256])
-@pytest.mark.parametrize("defer", [8, 32, 64])
+@pytest.mark.parametrize("defer", [8, 32, 64, 96])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(200, 300, 12, 0, 0), (48, 48, 14, 1, 1), (257, 100, 15, 1, 0)])
 def test_to_optimality(lpg, monkeypatch, wg, defer, m, n, seed, kind, rule, trade):
     assert _fits(m, n + m + 1, defer, wg)
@@ -92,12 +93,13 @@ def test_to_optimality(lpg, monkeypatch, wg, defer, m, n, seed, kind, rule, trad
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("defer", [15, 16, 17, 31, 33, 47, 48, 49, 63])
+@pytest.mark.parametrize("defer", [15, 16, 17, 31, 33, 47, 48, 49, 63, 64, 65, 79, 80, 81, 95, 96])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(300, 450, 21, 0, 0), (257, 300, 22, 1, 1)])
 def test_chain_batch_edges(lpg, monkeypatch, defer, m, n, seed, kind, rule):
     """The chains run in batches of 16 slots (lpg_block.hip chain<>): block
     sizes on either side of every batch edge, dense (Dantzig) and degenerate
-    (Bland: pivot rows that recur inside a block take the restart form)."""
+    (Bland: pivot rows that recur inside a block take the restart form); from
+    65 pending slots on the per-slot scalars take a second lane bank."""
     e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer)
     assert e.info.pivot_wg > 0
     o = Oracle(m, n + m + 1)
@@ -123,18 +125,21 @@ def test_config2_to_optimality(lpg, monkeypatch, wg):
     _assert_same(e, o, m)
 
 
-def test_runs_that_start_inside_a_block(lpg, monkeypatch):
+@pytest.mark.parametrize("defer", [64, 96])
+def test_runs_that_start_inside_a_block(lpg, monkeypatch, defer):
     """Enqueue 5, 9, 17, ... pivots: every launch after the first starts at a
-    pending index > 0 and reloads the earlier slots' slices from Pbuf / Cbuf;
-    a read in between flushes a partial block."""
-    m, n = 300, 450
-    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=64)
+    pending index > 0 and reloads the earlier slots' slices from Pbuf / Cbuf
+    (with 96-slot blocks also past slot 64, the second lane bank); a read in
+    between flushes a partial block."""
+    m, n = 600, 900
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer)
+    assert e.info.pivot_wg > 0
     o = Oracle(m, n + m + 1)
     e.generate(n, 77, 0)
     o.generate(n, 77, 0)
     e.reserve_log(4096)
     total = 0
-    for step in (5, 9, 17, 1, 33, 2, 64, 7):
+    for step in (5, 9, 17, 1, 33, 2, 64, 7, 70, 3, 90):
         e.enqueue(step, 0)
         total += step
         if step == 17:
@@ -145,10 +150,11 @@ def test_runs_that_start_inside_a_block(lpg, monkeypatch):
     _assert_same(e, o, m)
 
 
+@pytest.mark.parametrize("defer", [32, 96])
 @pytest.mark.parametrize("m,n,rule", [(257, 300, 0), (640, 512, 1)])
-def test_big_m_two_objective_rows(lpg, monkeypatch, m, n, rule):
+def test_big_m_two_objective_rows(lpg, monkeypatch, m, n, rule, defer):
     art_first = 1 + n + (m + 1) // 2
-    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32, flags=lpg._lib.FLAG_BIG_M)
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer, flags=lpg._lib.FLAG_BIG_M)
     assert e.info.pivot_wg > 0 and e.info.nobj == 2
     o = Oracle(m, n + m + 1, nobj=2)
     e.generate(n, 9, GEN_ARTIFICIAL)
@@ -161,12 +167,13 @@ def test_big_m_two_objective_rows(lpg, monkeypatch, m, n, rule):
     assert np.array_equal(e.get_rows(0, m + 2), o.get_rows())
 
 
+@pytest.mark.parametrize("defer", [64, 96])
 @pytest.mark.parametrize("m,n,piv", [(4096, 8192, 200), (2048, 20000, 150)])
-def test_same_as_two_kernel_pair(lpg, monkeypatch, m, n, piv):
+def test_same_as_two_kernel_pair(lpg, monkeypatch, m, n, piv, defer):
     """At sizes where the oracle is slow the persistent kernel is checked
     against the two-kernel pair: same log, same rows (sampled)."""
-    a = _engine(lpg, monkeypatch, m, n + m + 1, defer=64)
-    b = _engine(lpg, monkeypatch, m, n + m + 1, defer=64, persist=0)
+    a = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer)
+    b = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer, persist=0)
     assert a.info.pivot_wg > 0 and b.info.pivot_wg == 0
     for e in (a, b):
         e.generate(n, 5, 0)
