@@ -427,6 +427,24 @@ __device__ __forceinline__ double chain_n(const double *own, const double *uni, 
 }
 template <bool ROW, bool SEL, bool B2>
 __device__ __forceinline__ double chain(const double *own, const double *uni, int nb, int lim, double x) {
+#ifndef LPG_CHAIN_UNROLL96
+#ifdef LPG_CHAIN_LOOP64
+    if (true) {
+#else
+    if (B2) {
+#endif
+        // 96-slot blocks: a loop over pairs of batches (then one), not a fully
+        // unrolled form per batch count -- those six bodies per chain kind made
+        // the launch's code (77 KB) larger than the instruction cache two CUs
+        // share (64 KB); each pair restarts the operand prefetch (one LDS round
+        // trip per 32 slots)
+        int b = 0;
+#pragma unroll 1
+        for (; b + 2 <= nb; b += 2) x = chain_n<ROW, SEL, 2>(own + 16 * b, uni + 16 * b, lim - 16 * b, x);
+        if (b < nb) x = chain_n<ROW, SEL, 1>(own + 16 * b, uni + 16 * b, lim - 16 * b, x);
+        return x;
+    }
+#endif
     switch (nb) {      // nb <= KB / 16: blocks of <= 64 or <= 96 pivots (block_geometry)
         case 0: return x;
         case 1: return chain_n<ROW, SEL, 1>(own, uni, lim, x);

@@ -538,8 +538,15 @@ static int region_setup(lpg_ctx *c) {
 }
 
 // live columns and block-start basic columns for the current order and basis
-// (one workgroup, on the stream: no host sync); also clears DevState::rbad
+// (one workgroup, on the stream: no host sync); also clears DevState::rbad.
+// Always at a block boundary (a rebuild follows canonicalize / a bootstrap),
+// where Pbuf holds nothing pending: it is zeroed, because region mode keeps
+// the Pbuf entries of every column it does not hold at +0 (the block pass
+// skips all-zero tiles and reads the rest), and a column order restored by
+// canonicalize() leaves other columns' entries at the positions basic columns
+// now hold.
 static int region_build(lpg_ctx *c) {
+    HIPCHK(c, hipMemsetAsync(c->Pbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->ld * sizeof(double), c->stream));
     if (launch_region_build(lau(c), geo(c), c->st, c->basis, c->inv, c->mark, c->live, c->bcol0, c->ncols - 1 - c->m))
         return fail(c, LPG_ERR_DEVICE, "region build failed");
     c->reg_valid = true;

@@ -2274,17 +2274,22 @@ __global__ __launch_bounds__(kPlanNT) void k_swap_plan(DevState *__restrict__ st
     if (q == 0) pairs[0] = n;
 }
 
-// grid: (row blocks + 1, 4). One thread per row (constraint and objective
-// rows) and group of 16 pairs (blockIdx.y); the last x-block moves the
-// pending P entries.
+// grid: (row blocks + npb, 4). One thread per row (constraint and objective
+// rows) and group of 16 pairs (blockIdx.y); the last npb x-blocks move the
+// pending P entries, one (pending pivot, pair) per thread (a 96-pivot block
+// trades up to 96 pairs: 9,216 moves, which one block's loop of dependent
+// loads took ~40 us to make).
 __global__ __launch_bounds__(kBlock) void k_move_cols(double *__restrict__ T, Geo g, const DevState *__restrict__ st,
-                                                      double *__restrict__ Pbuf, const int32_t *__restrict__ pairs) {
+                                                      double *__restrict__ Pbuf, const int32_t *__restrict__ pairs,
+                                                      int npb) {
     const int n = pairs[0];
     if (n == 0) return;
-    if (blockIdx.x == gridDim.x - 1) {
-        if (blockIdx.y) return;
+    const int nrb = (int)gridDim.x - npb;
+    if ((int)blockIdx.x >= nrb) {
         const int np = (int)st->npend;
-        for (int e = threadIdx.x; e < np * n; e += kBlock) {
+        const int nt = npb * (int)gridDim.y * kBlock;
+        for (int e = (((int)blockIdx.x - nrb) * (int)gridDim.y + (int)blockIdx.y) * kBlock + threadIdx.x; e < np * n;
+             e += nt) {
             const int q = e / n, p = e - q * n;
             double *Pq = Pbuf + (int64_t)q * g.ld;
             const int32_t a = pairs[1 + 3 * p], b = pairs[2 + 3 * p];
@@ -2336,11 +2341,11 @@ __global__ __launch_bounds__(kBlock) void k_move_cols(double *__restrict__ T, Ge
 __device__ __forceinline__ void end_block(DevState *st, const Defer &D, int kmax, bool spare_zero = false,
                                           int64_t ld = 0) {
     const int q = threadIdx.x;
-    if (spare_zero) {
-        for (int e = q; e < kmax * kmax; e += blockDim.x) {
-            const int qq = e / kmax, u = e - qq * kmax;
-            const int64_t L = D.lv[qq];
-            if (L > 0) D.Pbuf[(int64_t)u * ld + D.inv[L]] = 0.0;
+    if (spare_zero) {              // one leaving column per thread: its kmax entries, no dependent load inside
+        const int64_t L = q < kmax ? D.lv[q] : 0;
+        if (L > 0) {
+            double *col = D.Pbuf + D.inv[L];
+            for (int u = 0; u < kmax; u++) col[(int64_t)u * ld] = 0.0;
         }
         __syncthreads();
     }
@@ -2390,8 +2395,9 @@ int launch_swap_plan(const Launch &L, const Geo &g, DevState *st, const Defer &D
 
 int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs) {
     const int64_t rows = g.nloc + g.nobj;
-    hipLaunchKernelGGL(k_move_cols, dim3((unsigned)((rows + kBlock - 1) / kBlock + 1), 4), dim3(kBlock), 0,
-                       (hipStream_t)L.stream, g.T, g, st, D.Pbuf, pairs);
+    const int npb = (LPG_DEFER_MAX * LPG_DEFER_MAX + 4 * kBlock - 1) / (4 * kBlock);   // one move per thread at the most
+    hipLaunchKernelGGL(k_move_cols, dim3((unsigned)((rows + kBlock - 1) / kBlock + npb), 4), dim3(kBlock), 0,
+                       (hipStream_t)L.stream, g.T, g, st, D.Pbuf, pairs, npb);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2453,6 +2459,12 @@ int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &
     const int64_t ntiles_p = (g.ncols + 63) / 64;   // k_flush_pivot_rows column tiles
     // (96-slot blocks take the 128-slot form: a 96-slot instance, two blocks
     // per CU, measured 0.2% slower at config 4, profiles/r04_ab_pivrows96.log)
+#ifdef LPG_PIVROWS96
+    if (kmax == 96)
+        hipLaunchKernelGGL(k_flush_pivot_rows<96>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
+                           D.Pbuf, D.mul, D.rq);
+    else
+#endif
     if (kmax > 64)
         hipLaunchKernelGGL(k_flush_pivot_rows<128>, dim3((unsigned)ntiles_p), dim3(kBlock), 0, stream, g.T, g, st,
                            D.Pbuf, D.mul, D.rq);

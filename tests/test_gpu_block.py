@@ -79,10 +79,11 @@ def test_engaged_where_the_slices_fit(lpg, monkeypatch):
 @pytest.mark.parametrize("defer", [8, 32, 64, 96])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(200, 300, 12, 0, 0), (48, 48, 14, 1, 1), (257, 100, 15, 1, 0)])
 def test_to_optimality(lpg, monkeypatch, wg, defer, m, n, seed, kind, rule, trade):
-    assert _fits(m, n + m + 1, defer, wg)
     monkeypatch.setenv("LPG_NO_REORDER", "0" if trade == "1" else "1")
     e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer, wg=wg)
-    assert e.info.pivot_wg > 0
+    if e.info.pivot_wg == 0 and not _fits(m, n + m + 1, defer, wg):
+        pytest.skip("this split holds neither the all-column nor the region slices")
+    assert e.info.pivot_wg > 0 and e.info.region == (1 if trade == "1" else 0)
     o = Oracle(m, n + m + 1)
     e.generate(n, seed, kind)
     o.generate(n, seed, kind)

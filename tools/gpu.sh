@@ -9,7 +9,7 @@
 #   pmc:NAME:CTR:ARGS  one rocprofv3 --pmc pass (CTR) of bench.py ARGS -> gpurun_out/pmc_NAME/
 #   py:NAME:ARGS       python ARGS                   -> gpurun_out/py_NAME.log
 #   smoke:NAME:        __graft_entry__.smoke()       -> gpurun_out/smoke_NAME.log
-#   ab:NAME:LIBS       config-3 pivots/s of the in-tree liblpg and each .so in LIBS,
+#   ab:NAME:VARIANTS   config-3 pivots/s of each variant ("[LIB] [NAME=VALUE ...]", ';'-separated),
 #                      interleaved twice (tools/sweep_exp.py) -> gpurun_out/ab_NAME.log
 #   run:NAME:CMD       any other command (lab binaries such as tools/flush_lab,
 #                      env-var sweeps: "run:x:env LPG_DEFER=32 python bench.py")
@@ -55,10 +55,15 @@ for spec in "$@"; do
                 || { tail -20 "gpurun_out/smoke_$name.log"; exit 1; }
             tail -2 "gpurun_out/smoke_$name.log" ;;
         ab)
+            # ARGS: variants separated by ';', each "[LIB] [NAME=VALUE ...]" (empty: the in-tree
+            # build as it is), run twice, interleaved (tools/sweep_exp.py)
             : > "gpurun_out/ab_$name.log"
-            for lib in "" $args "" $args; do
-                timeout -k 10 "${T_PY:-300}" python -u tools/sweep_exp.py $lib >> "gpurun_out/ab_$name.log" 2>&1 \
-                    || { tail -30 "gpurun_out/ab_$name.log"; exit 1; }
+            IFS=';' read -ra vars <<< "$args"
+            for rep in 1 2; do
+                for v in "${vars[@]}"; do
+                    timeout -k 10 "${T_PY:-300}" python -u tools/sweep_exp.py $v >> "gpurun_out/ab_$name.log" 2>&1 \
+                        || { tail -30 "gpurun_out/ab_$name.log"; exit 1; }
+                done
             done
             grep pivots/s "gpurun_out/ab_$name.log" ;;
         run)
