@@ -787,8 +787,10 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             if (actnow) bc0 = a.bcol0[rs];               // {logical, physical}: needed from the next pivot on
         }
         const double xrow = (owns && hc) ? g.T[rloc * g.ld + c] : (actnow ? 1.0 : 0.0);
-        const double mrow = (owns && lane < q) ? -ld_wt(D.Cbuf + (int64_t)lane * D.cs + rloc) : -0.0;
-        const double mrow1 = (B2 && owns && 64 + lane < q) ? -ld_wt(D.Cbuf + (int64_t)(64 + lane) * D.cs + rloc) : -0.0;
+        // (unconditional loads from clamped addresses, negated and selected at
+        // their use: a load behind the condition was waited for on the spot)
+        const double mraw = ld_wt(D.Cbuf + (int64_t)(lane < q ? lane : 0) * D.cs + (owns ? rloc : 0));
+        const double mraw1 = B2 ? ld_wt(D.Cbuf + (int64_t)(64 + lane < q ? 64 + lane : 0) * D.cs + (owns ? rloc : 0)) : 0.0;
         if (RPIV && pvneed) {
             // the winner's {piv, row} granule: stored with its {theta, row}, so
             // normally already visible; re-polled (bounded) if not
@@ -831,8 +833,8 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         // the multipliers -C_u[rr] (lane u < q; -0 past q), the restart point
         // (the last pending pivot on rr), the base entries, the pending chain
         auto pivot_row = [&](bool on, int64_t rr) -> double {
-            wm[wave][lane] = mrow;
-            if (B2 && lane < 32) wm[wave][64 + lane] = mrow1;
+            wm[wave][lane] = (owns && lane < q) ? -mraw : -0.0;
+            if (B2 && lane < 32) wm[wave][64 + lane] = (owns && 64 + lane < q) ? -mraw1 : -0.0;
             const unsigned long long hit = __ballot(on && lane < q && rqv == rr);
             const unsigned long long hit1 = B2 ? __ballot(on && 64 + lane < q && rqv1 == rr) : 0ull;
             const int qs = hit1 ? 127 - __clzll((long long)hit1) : (hit ? 63 - __clzll((long long)hit) : -1);
@@ -911,9 +913,13 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         int64_t lvv = 0;                                // MR: the leaving variable, from the replicated basis
         // k_prep_d's bookkeeping, stores only (a dependent load here would hold
         // back workgroup 0, and every sweep waits for the slowest workgroup):
-        // the row's owner records the leaving variable it holds
-        // (moving it to wave 1 after the pricing record measured nothing)
-        if (wg == 0 && tid == 0) {
+        // the row's owner records the leaving variable it holds. One rank:
+        // both after this pivot's pricing record (book_late below) -- here they
+        // sat in front of the drain that gates the record, and workgroup 0 was
+        // the last to publish in 43 of 64 pivots (profiles/r04_block_probe_clock.log)
+        const bool own_row = hr && i == rl;             // this thread holds the leaving row
+        const int64_t lv_old = mybasis;
+        if (MR && wg == 0 && tid == 0) {
             st->slot[s].r = r;
             D.rq[q] = rl;
             if (MR) lvv = D.basis[r];                   // stored after the P exchange: its latency hides there
@@ -929,11 +935,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             st->last_k = kt;
             st->last_r = r;
         }
-        if (hr && i == rl) {
-            if (!MR) {
-                D.lv[q] = mybasis;
-                D.basis[r] = kt;
-            }
+        if (own_row) {
             mybasis = kt;
             lastpiv = q;
         }
@@ -1034,6 +1036,27 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             for (int k = 1; k < NGP; k++) rec_store(recP, (wg * NGP + k) * 16, pack(0ull, 0u, tag));
         }
         LPG_BPUB(0, t);
+        if (!MR) {                                      // book_late: nobody in this launch reads these
+            if (wg == 0 && tid == 64) {
+                st->slot[s].r = r;
+                D.rq[q] = rl;
+                st->npend = q + 1;
+                D.kq[q] = kt;
+                D.pv[q] = piv;
+                const int64_t np = np0 + t;
+                if (D.logk && np < logcap) {
+                    D.logk[np] = kt;
+                    D.logr[np] = r;
+                }
+                st->pivots = np + 1;
+                st->last_k = kt;
+                st->last_r = r;
+            }
+            if (own_row) {
+                D.lv[q] = lv_old;
+                D.basis[r] = kt;
+            }
+        }
         LPG_BPH(t, 3);
 
         // ================= phase S: the entering column and the ratio test
@@ -1236,7 +1259,10 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             }
         }
         LPG_BPH(t, 13);
-        cd = block_argmin_cand<kNT / 64, false>(cd);
+        // all rows in wave 0 (rw <= 64, config 3): its own wave min, no LDS
+        // exchange and no barrier (the other waves hold no candidate)
+        if (rw <= 64) cd = wave == 0 ? block_argmin_cand<1, false>(cd) : cd;
+        else cd = block_argmin_cand<kNT / 64, false>(cd);
         LPG_BPH(t, 14);
         if (tid == 0) {
             uint64_t h = ~0ull;

@@ -149,14 +149,23 @@ __device__ __forceinline__ uint64_t dpp64(uint64_t v) {
 }
 __device__ __forceinline__ uint64_t min64(uint64_t a, uint64_t b) { return b < a ? b : a; }
 
+// the same move where every lane of every row takes a source lane (quad_perm,
+// mirrors): no old value to keep, so no copy in front of the DPP move
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64f(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, true);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // minimum over the wave, in lane 63: four steps within each 16-lane row,
 // then row_bcast:15 (rows 1, 3 take lane 15 of the row below) and
 // row_bcast:31 (rows 2, 3 take lane 31)
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t m) {
-    m = min64(m, dpp64<0xB1>(m));          // quad_perm [1,0,3,2]: lane ^ 1
-    m = min64(m, dpp64<0x4E>(m));          // quad_perm [2,3,0,1]: lane ^ 2
-    m = min64(m, dpp64<0x141>(m));         // row_half_mirror
-    m = min64(m, dpp64<0x140>(m));         // row_mirror
+    m = min64(m, dpp64f<0xB1>(m));         // quad_perm [1,0,3,2]: lane ^ 1
+    m = min64(m, dpp64f<0x4E>(m));         // quad_perm [2,3,0,1]: lane ^ 2
+    m = min64(m, dpp64f<0x141>(m));        // row_half_mirror
+    m = min64(m, dpp64f<0x140>(m));        // row_mirror
     m = min64(m, dpp64<0x142, 0xA>(m));    // row_bcast:15
     m = min64(m, dpp64<0x143, 0xC>(m));    // row_bcast:31
     return rdl64(m, 63);
@@ -166,11 +175,15 @@ template <int CTRL, int ROWMASK = 0xF>
 __device__ __forceinline__ uint32_t dpp32m(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROWMASK, 0xF, false);
 }
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32f(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t m) {
-    m = min(m, dpp32m<0xB1>(m));
-    m = min(m, dpp32m<0x4E>(m));
-    m = min(m, dpp32m<0x141>(m));
-    m = min(m, dpp32m<0x140>(m));
+    m = min(m, dpp32f<0xB1>(m));
+    m = min(m, dpp32f<0x4E>(m));
+    m = min(m, dpp32f<0x141>(m));
+    m = min(m, dpp32f<0x140>(m));
     m = min(m, dpp32m<0x142, 0xA>(m));
     m = min(m, dpp32m<0x143, 0xC>(m));
     return rdl32(m, 63);

@@ -1,9 +1,11 @@
 """Parity at BASELINE.json's full sizes (configs 3, 4 and 5), on the device.
 
-* config 3 (16384 x 32768): 200 pivots = three whole deferred blocks of 64
+* config 3 (16384 x 32768): three whole deferred blocks of 96 (the default)
+  or 64 pivots plus 8
   (each ending in the column trade k_swap_plan / k_move_cols / k_fill_cols,
   the block pass k_flushw over reordered columns and the pivot-row rewrite
-  k_flush_pivot_rows) plus 8 pending pivots flushed by the readout; bitwise
+  k_flush_pivot_rows; the pivots in the region-mode persistent launch)
+  plus 8 pending pivots flushed by the readout; bitwise
   against the C oracle: pivot log, basis, column 0, objective row, every pivot
   row and 64 sampled rows; basic columns are unit vectors on those rows.
 * config 5 (two-phase, Bland, m = n = 8192, KM-style degenerate with
@@ -52,23 +54,30 @@ def _log(x):
     return list(zip(k.tolist(), r.tolist()))
 
 
-def test_config3_three_blocks_bitwise(lpg):
+@pytest.mark.parametrize("defer", [None, 64])
+def test_config3_three_blocks_bitwise(lpg, defer, monkeypatch):
+    """The default (96-pivot blocks, the region-mode persistent launch) and
+    64-pivot blocks: three whole blocks and a partial one of 8."""
     m, n = 16384, 32768
+    if defer:
+        monkeypatch.setenv("LPG_DEFER", str(defer))
     e = lpg.Engine(m, n + m + 1)
-    assert e.info.defer_k == 64
+    monkeypatch.delenv("LPG_DEFER", raising=False)
+    K = e.info.defer_k
+    assert K == (defer or 96) and e.info.pivot_wg > 0 and e.info.region == 1
     e.generate(n, SEED, lpg.GEN_DENSE)
-    e.reserve_log(256)
-    e.enqueue(64, lpg.RULE_DANTZIG)          # block 1 (the replayed graph is built after it)
+    e.reserve_log(3 * K + 16)
+    e.enqueue(K, lpg.RULE_DANTZIG)           # block 1
     e.prepare(lpg.RULE_DANTZIG)
-    e.enqueue(128, lpg.RULE_DANTZIG)         # blocks 2 and 3, replayed
+    e.enqueue(2 * K, lpg.RULE_DANTZIG)       # blocks 2 and 3
     mid = e.sync()
-    assert mid.pivots == 192
+    assert mid.pivots == 3 * K
     res = e.solve(8, lpg.RULE_DANTZIG)       # 8 more: a partial block, flushed by the readout
-    assert res.status_name == "ITER_LIMIT" and res.pivots == 200
+    assert res.status_name == "ITER_LIMIT" and res.pivots == 3 * K + 8
     o = _oracle(m, n + m + 1)
     o.generate(n, SEED, 0)
-    ores = o.solve(200, 0)
-    assert ores.pivots == 200 and res.objective == ores.objective
+    ores = o.solve(3 * K + 8, 0)
+    assert ores.pivots == 3 * K + 8 and res.objective == ores.objective
     log = _log(e)
     assert log == _log(o)
     basis = e.get_basis()
