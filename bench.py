@@ -49,6 +49,29 @@ import torch.distributed as dist  # noqa: E402
 ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "Simplex pivots/sec + HBM GB/s fraction, dense m=16384×n=32768 fp64, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# dense f64 matrix-core peak of MI355X (AMD's published FP64 matrix figure, no
+# sparsity; 256 CUs x 4 SIMDs x 32 flop/clk x 2.4 GHz); the box's f64 MFMA pipe
+# measures 73-75 TFLOP/s in isolation (profiles/r01_mfma_rate.log)
+MFMA_F64_PEAK_TFS = 78.6
+
+
+def roofline_bound(touched, defer, upd_ms):
+    """The block pass against both rooflines: HBM (16 B per live element,
+    touched = bytes per launch) and the f64 matrix cores (2 flops per live
+    element per pending pivot). `bound` is the one whose ideal time is longer
+    (HBM below ~78 pending pivots, the matrix cores above: 16 x 78.6 / 8000 x 8
+    ~ 77 flop per byte pair); `achieved` / `frac` are that roofline's."""
+    flops = touched / 16.0 * 2.0 * max(defer, 1)
+    t = upd_ms * 1e-3 if upd_ms > 0 else float("inf")
+    hbm = {"achieved": touched / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    hbm["frac"] = hbm["achieved"] / HBM_PEAK_GBS
+    mf = {"achieved": flops / t / 1e12, "peak": MFMA_F64_PEAK_TFS, "unit": "TFLOP/s",
+          "algorithmic_flops_per_launch": flops}
+    mf["frac"] = mf["achieved"] / MFMA_F64_PEAK_TFS
+    t_hbm, t_mf = touched / (HBM_PEAK_GBS * 1e9), flops / (MFMA_F64_PEAK_TFS * 1e12)
+    main, bound = (mf, "mfma") if t_mf > t_hbm else (hbm, "hbm")
+    return {"bound": bound, "achieved": main["achieved"], "peak": main["peak"], "unit": main["unit"],
+            "frac": main["frac"], "hbm": hbm, "mfma": mf}
 SEED = 20220518
 CONFIGS = {
     2: dict(m=1024, n=2048, name="BASELINE config 2: random dense LP m=1024 n=2048 fp64"),
@@ -408,8 +431,8 @@ def main():
     achieved = touched / (upd_ms * 1e-3) / 1e9 if upd_ms > 0 else 0.0
     kname = ("k_flushw" if lpg.flush_kernel_for(defer) == "w" else "k_flushm") if defer else "k_update"
     ms_block = elapsed * 1e3 / max(done, 1) * K
-    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+    roof = roofline_bound(touched, defer, upd_ms)
+    roof.update({"traffic": None,
             "kernel": f"lpg::{kname}" + (f" (Gauss-Jordan block pass, {defer} pending pivots per launch; HIP events "
                                          f"around this kernel alone)" if defer else " (Gauss-Jordan rank-1)"),
             "pending_pivots_per_launch": defer or 1,
@@ -417,15 +440,17 @@ def main():
             "algorithmic_bytes_per_launch": touched,
             "full_tableau_bytes_per_launch": info.bytes_per_pivot,
             "column_skipping": not a.no_skip,
-            "update_ms_mean": upd_ms}
+            "update_ms_mean": upd_ms})
     if defer and live_events:
         # per-block ceiling: the pass at the HBM spec peak plus the measured rest of the block (pivot kernels,
         # column trade, pivot-row rewrite, launch gaps), i.e. what this design reaches with a perfect pass
         other_ms = ms_block - upd_ms
-        ceil_ms = touched / (HBM_PEAK_GBS * 1e9) * 1e3 + other_ms
-        roof.update({"ms_per_block": ms_block, "other_ms_per_block": other_ms,
+        pass_ideal_ms = max(touched / (HBM_PEAK_GBS * 1e9), roof["mfma"]["algorithmic_flops_per_launch"] /
+                            (MFMA_F64_PEAK_TFS * 1e12)) * 1e3
+        ceil_ms = pass_ideal_ms + other_ms
+        roof.update({"ms_per_block": ms_block, "other_ms_per_block": other_ms, "pass_ideal_ms": pass_ideal_ms,
                      "block_ceiling_ms": ceil_ms, "block_ceiling_pivots_per_s": defer / (ceil_ms * 1e-3),
-                     "pass_only_ceiling_pivots_per_s": defer / (touched / (HBM_PEAK_GBS * 1e9))})
+                     "pass_only_ceiling_pivots_per_s": defer / (pass_ideal_ms * 1e-3)})
     stamp = source_stamp()
     roof["source_stamp"] = stamp
     p, why = pmc_traffic(a, kname, defer, m, n, world, stamp)

@@ -1372,9 +1372,12 @@ int block_geometry_region(const Geo &g, int ks, int cus, int want, int64_t nlive
 
 // live: the physical columns in [1, ncols) holding no basic variable, ascending;
 // bcol0[r] = (basis[r] << 32) | its physical column; rbad cleared. mark: ld ints.
+// tlive[c] = 1 iff the 64 physical columns 64c .. 64c+63 hold a nonbasic one
+// (column 0 included): the block pass skips a tile with none without reading
+// its pending P entries (k_flushw), checking only the block's leaving columns.
 __global__ __launch_bounds__(1024) void k_region_build(DevState *st, const int64_t *basis, const int32_t *inv,
-                                                        int64_t m, int64_t ncols, int32_t *mark, int32_t *live,
-                                                        int64_t *bcol0, int64_t nlive) {
+                                                        int64_t m, int64_t ncols, int64_t ld, int32_t *mark,
+                                                        int32_t *live, int64_t *bcol0, int64_t nlive, int32_t *tlive) {
     const int tid = threadIdx.x, nt = blockDim.x;
     for (int64_t p = tid; p < ncols; p += nt) mark[p] = 0;
     __syncthreads();
@@ -1385,6 +1388,11 @@ __global__ __launch_bounds__(1024) void k_region_build(DevState *st, const int64
         bcol0[r] = (v << 32) | (int64_t)(uint32_t)p;
     }
     __syncthreads();
+    for (int64_t c = tid; c < ld / 64; c += nt) {
+        int any = 0;
+        for (int64_t p = 64 * c; p < 64 * c + 64 && p < ncols; p++) any |= mark[p] == 0;
+        tlive[c] = any;
+    }
     // stable compaction of the unmarked columns 1..ncols-1: each thread a contiguous chunk
     const int64_t per = (ncols - 1 + nt - 1) / nt, p0 = 1 + (int64_t)tid * per, p1 = std::min<int64_t>(p0 + per, ncols);
     int cnt = 0;
@@ -1422,9 +1430,10 @@ __global__ __launch_bounds__(256) void k_region_check(const double *T, Geo g, co
 }
 
 int launch_region_build(const Launch &L, const Geo &g, DevState *st, const int64_t *basis, const int32_t *inv,
-                        int32_t *mark, int32_t *live, int64_t *bcol0, int64_t nlive) {
+                        int32_t *mark, int32_t *live, int64_t *bcol0, int64_t nlive, int32_t *tlive) {
+    if (g.ld % 64) return -1;
     hipLaunchKernelGGL(k_region_build, dim3(1), dim3(1024), 0, (hipStream_t)L.stream, st, basis, inv, g.m, g.ncols,
-                       mark, live, bcol0, nlive);
+                       g.ld, mark, live, bcol0, nlive, tlive);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -82,6 +82,9 @@ struct lpg_ctx {
     bool units_known = false;
     RegionGeo rg{};
     int32_t *live = nullptr, *mark = nullptr;
+    int32_t *tlive = nullptr;     // region: 64-column chunks holding a block-start nonbasic column (k_flushw skips the rest)
+    bool block_region = false;    // the pending block's pivots ran in region mode (its flush may use tlive)
+    bool tlive_on = true;         // LPG_FLUSH_TLIVE=0: the pass reads every tile's P entries (A/B)
     int64_t *bcol0 = nullptr;
     int *rok = nullptr;           // region_check's flag
     void *rec = nullptr;          // its records (zeroed once; tags never repeat within a context)
@@ -111,6 +114,7 @@ struct lpg_ctx {
     int defer_k = 0;
     int pend = 0;                 // pivots enqueued since the last flush (host view)
     int flush_variant = -1;       // launch_flush_main `which`: -1 default, 0 k_flushm, 1 k_flushw
+    int flush_xcd = -1;           // launch_flush_main `xcd`: -1 auto, 0 global queue, 1 XCD-grouped
     bool capture_block = false;   // capturing a deferred block's pivots (its flush stays outside the graph)
     bool fast_pivot = true;       // deferred single-rank pivots through k_prep_d / k_select_d (LPG_SLOW_PIVOT=1: generic pair)
     double *Pbuf = nullptr, *Cbuf = nullptr;
@@ -386,7 +390,11 @@ static int flush_launch(lpg_ctx *c) {
         (re && launch_move_cols(lau(c), geo(c), c->st, defer_of(c, 0), c->pairs)))
         return fail(c, LPG_ERR_DEVICE, "swap plan launch failed");
     if (c->timing && ((rc = timing_mark(c, 0)) || (rc = timing_mark(c, 1)))) return rc;
-    if (launch_flush_main(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, c->skip, c->flush_variant))
+    // tlive: region blocks only (every pivot recorded its leaving column, the
+    // basic columns were exact unit vectors at the block start); LPG_FLUSH_TLIVE=0 off (A/B)
+    const int32_t *tl = (c->block_region && c->reg_valid && re && c->tlive_on && c->skip) ? c->tlive : nullptr;
+    c->block_region = false;
+    if (launch_flush_main(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, c->skip, c->flush_variant, c->flush_xcd, tl))
         return fail(c, LPG_ERR_DEVICE, "flush launch failed");
     if (c->timing && (rc = timing_mark(c, 2, 2))) return rc;
     if (launch_flush_tail(lau(c), geo(c), c->st, defer_of(c, 0), c->pend, !re))
@@ -547,7 +555,8 @@ static int region_setup(lpg_ctx *c) {
 // now hold.
 static int region_build(lpg_ctx *c) {
     HIPCHK(c, hipMemsetAsync(c->Pbuf, 0, (size_t)flush_kmax_supported(c->defer_k) * c->ld * sizeof(double), c->stream));
-    if (launch_region_build(lau(c), geo(c), c->st, c->basis, c->inv, c->mark, c->live, c->bcol0, c->ncols - 1 - c->m))
+    if (launch_region_build(lau(c), geo(c), c->st, c->basis, c->inv, c->mark, c->live, c->bcol0, c->ncols - 1 - c->m,
+                            c->tlive))
         return fail(c, LPG_ERR_DEVICE, "region build failed");
     c->reg_valid = true;
     return 0;
@@ -598,6 +607,7 @@ static int enqueue_blocks(lpg_ctx *c, int64_t npiv, int rule) {
                                                  mr ? &X : nullptr, c->xtag) == 0;
         if (!ok)
             return fail(c, LPG_ERR_DEVICE, "pivot block launch failed");
+        if (reg) c->block_region = true;
         c->pb_launch++;
         if (mr) {
             c->xtag += (uint32_t)n;
@@ -1051,6 +1061,15 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
 #endif
     const char *fv = getenv("LPG_FLUSH_KERNEL");   // m | w: force k_flushm / k_flushw (tests); default by block size
     c->flush_variant = fv ? (fv[0] == 'w' ? 1 : fv[0] == 'm' ? 0 : -1) : -1;
+    // 0 | 1 | h1, h2, h4, h8: k_flushw's global / XCD-grouped item queue, the
+    // latter with H column classes (tests, A/B); unset: by size
+    const char *ft = getenv("LPG_FLUSH_TLIVE");
+    c->tlive_on = !(ft && ft[0] == '0');
+    const char *fx = getenv("LPG_FLUSH_XCD");
+    c->flush_xcd = -1;
+    if (fx && fx[0] == '0') c->flush_xcd = 0;
+    if (fx && fx[0] == '1') c->flush_xcd = 1;
+    if (fx && fx[0] == 'h' && (fx[1] == '1' || fx[1] == '2' || fx[1] == '4' || fx[1] == '8')) c->flush_xcd = 10 + (fx[1] - '0');
     int rc;
     if ((rc = use_device(c))) { lpg_destroy(c); return rc; }
     const int64_t rows = c->nloc + c->nobj;
@@ -1109,6 +1128,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     if (c->reg) {
         ALLOC(c->live, (size_t)ncols * sizeof(int32_t));
         ALLOC(c->mark, (size_t)c->ld * sizeof(int32_t));
+        ALLOC(c->tlive, (size_t)(c->ld / 64 + 1) * sizeof(int32_t));
         ALLOC(c->bcol0, (size_t)m * sizeof(int64_t));
         ALLOC(c->rok, sizeof(int));
     }
@@ -1383,7 +1403,7 @@ void lpg_destroy(lpg_ctx *c) {
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
                     c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->mul, c->pv, c->tmp,
-                    c->rec, c->drc, c->dcp, c->drc_all, c->live, c->mark, c->bcol0, c->rok};
+                    c->rec, c->drc, c->dcp, c->drc_all, c->live, c->mark, c->bcol0, c->rok, c->tlive};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);

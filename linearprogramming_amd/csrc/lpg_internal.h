@@ -61,6 +61,7 @@ struct DevState {
     uint32_t rbad;                // region mode invalid: 1 a block's column trade was incomplete (k_swap_plan),
                                   // 2 the region build found no m distinct basic columns; 0 once rebuilt
     uint32_t pad1;
+    unsigned long long gwork[8];  // k_flushw's per-XCD-group dequeue heads (FlushX; reset with fwork)
 };
 constexpr int64_t kStallResidency = 4;
 constexpr int64_t kStallPending = 5;
@@ -209,7 +210,9 @@ int block_geometry(const Geo &g, int ks, int cus, int want, int *nwg, int *cw, i
 // columns of the block start (live, column 0 excluded) plus per pending pivot
 // one spare slot for the column leaving the basis then, and column 0 (lpg_block.hip
 // k_pivot_block). block_geometry_region picks the split; launch_region_build
-// (one workgroup) writes live and bcol0 from the basis and clears rbad;
+// (one workgroup) writes live, bcol0 and the 64-column liveness map tlive
+// (ld / 64 ints: the block pass skips tiles without a nonbasic column, see
+// launch_flush_main) from the basis and clears rbad;
 // launch_region_check clears ok[0] unless every basic column is an exact unit
 // vector with a zero reduced cost (the region's precondition).
 struct RegionGeo {
@@ -224,7 +227,7 @@ struct RegionArgs {
 };
 int block_geometry_region(const Geo &g, int ks, int cus, int want, int64_t nlive, RegionGeo *out);
 int launch_region_build(const Launch &L, const Geo &g, DevState *st, const int64_t *basis, const int32_t *inv,
-                        int32_t *mark, int32_t *live, int64_t *bcol0, int64_t nlive);
+                        int32_t *mark, int32_t *live, int64_t *bcol0, int64_t nlive, int32_t *tlive);
 int launch_region_check(const Launch &L, const Geo &g, const int64_t *basis, const int32_t *inv, int *ok);
 int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, int s0, int q0, int n, Cand *part,
                        int ncand, const Cand *cin, int ncin, const double *Cs0, double *Cs1, const Defer &D,
@@ -235,7 +238,17 @@ int launch_flush(const Launch &L, const Geo &g, DevState *st, const Defer &D, in
 // ... in two parts: the block pass itself (k_flushw / k_flushm / k_flush), then
 // the pivot-row rewrite and the pending-counter reset (the rewrite's
 // multipliers come from launch_swap_plan, launched before either part)
-int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which);
+// xcd: k_flushw's item map, -1 auto, 0 the global queue, 1 the XCD-grouped one (FlushX),
+// 10 + H the latter with H column classes.
+// tlive (region mode, launch_region_build's map, or null): a tile none of
+// whose 64-column chunks holds a block-start nonbasic column and none of whose
+// columns is a leaving column of the block (D.lv through D.inv, after the
+// trade) has all-zero pending P entries and is skipped without reading them.
+// Valid only for a block whose P entries of other columns are +-0: the basic
+// columns were exact unit vectors at the block start (region mode's check)
+// and every pivot recorded its leaving variable in D.lv.
+int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which,
+                      int xcd = -1, const int32_t *tlive = nullptr);
 // reset = false: the caller ends the block itself (launch_fill_cols with st)
 int launch_flush_tail(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, bool reset = true);
 // Item map of the banded block pass (k_flushw): column tile
@@ -269,6 +282,66 @@ __host__ __device__ inline void flush_item(int64_t item, int64_t ntiles, int64_t
         i1 = i0 + tr;
     }
     if (i1 > nloc) i1 = nloc;
+}
+// XCD-grouped item map of k_flushw: the persistent blocks b with the same
+// b % 8 share one XCD (one L2), and group g = b % 8 dequeues from its own
+// queue (DevState::gwork[g]) the items of one row band x column class: band
+// g / H of 8 / H bands, tiles t = h + H j of class h = g % H. Within a group the
+// items run sub-band by sub-band (rs rows, the band's multipliers C held in
+// that XCD's L2), tiles in descending order, and the last sub-band's lowest tt
+// tiles are cut into nq row pieces each, one tile's pieces in a row (its P
+// tile stays in L2), so the queue ends on short items where the column trade
+// keeps the live columns. A group whose queue is empty takes items from the
+// others (g + 1, g + 2, ...): every item is run once whatever the placement.
+struct FlushX {
+    int64_t ntiles, nloc;
+    int32_t H;        // column classes (1, 2, 4, 8)
+    int32_t rb;       // band rows (multiple of 16)
+    int32_t rs;       // sub-band rows (multiple of 16, <= rb)
+    int32_t tt;       // tail tiles per group
+    int32_t on;
+    int32_t pad;
+};
+struct FlushXGroup {
+    int64_t r0, r1, ntg, nsb, ttg, nq, qrows, count;
+};
+__host__ __device__ inline FlushXGroup flushx_group(const FlushX &f, int g) {
+    FlushXGroup o{};
+    const int b = g / f.H, h = g % f.H;
+    o.r0 = (int64_t)b * f.rb;
+    o.r1 = o.r0 + f.rb < f.nloc ? o.r0 + f.rb : f.nloc;
+    o.ntg = h < f.ntiles ? (f.ntiles - h + f.H - 1) / f.H : 0;
+    if (o.r0 >= f.nloc || o.ntg == 0) return o;
+    o.nsb = (o.r1 - o.r0 + f.rs - 1) / f.rs;
+    const int64_t ls = (o.r1 - o.r0) - (o.nsb - 1) * f.rs;   // last sub-band's rows
+    o.qrows = ((ls + 3) / 4 + 15) / 16 * 16;
+    o.nq = (ls + o.qrows - 1) / o.qrows;
+    o.ttg = f.tt < o.ntg ? f.tt : o.ntg;
+    o.count = (o.nsb - 1) * o.ntg + (o.ntg - o.ttg) + o.nq * o.ttg;
+    return o;
+}
+__host__ __device__ inline void flushx_item(const FlushX &f, const FlushXGroup &G, int g, int64_t it, int64_t &tile,
+                                            int64_t &i0, int64_t &i1) {
+    const int h = g % f.H;
+    int64_t j;
+    const int64_t full = (G.nsb - 1) * G.ntg;
+    const int64_t base = G.r0 + (G.nsb - 1) * f.rs;
+    if (it < full) {
+        j = G.ntg - 1 - it % G.ntg;
+        i0 = G.r0 + (it / G.ntg) * f.rs;
+        i1 = i0 + f.rs;
+    } else if (it - full < G.ntg - G.ttg) {
+        j = G.ntg - 1 - (it - full);
+        i0 = base;
+        i1 = G.r1;
+    } else {
+        const int64_t k = it - full - (G.ntg - G.ttg);
+        j = G.ttg - 1 - k / G.nq;
+        i0 = base + (k % G.nq) * G.qrows;
+        i1 = i0 + G.qrows;
+    }
+    if (i1 > G.r1) i1 = G.r1;
+    tile = h + (int64_t)f.H * j;
 }
 int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0: k too large)
 // Basis-partitioned column order (single-rank deferred path): after a block,

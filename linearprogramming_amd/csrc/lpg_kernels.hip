@@ -1872,7 +1872,10 @@ template <int KMAX, int NB, int LB, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T, Geo g, DevState *__restrict__ st,
                                                          const double *__restrict__ Pbuf,
                                                          const double *__restrict__ Cbuf, int64_t cs, int64_t ntiles,
-                                                         int64_t nitems, int64_t rows, int skip) {
+                                                         int64_t nitems, int64_t rows, int skip, FlushX X,
+                                                         const int32_t *__restrict__ tlive,
+                                                         const int64_t *__restrict__ lv,
+                                                         const int32_t *__restrict__ inv) {
     constexpr int NTH = 64 * WPB;
     constexpr int G = KMAX / 4;
     constexpr int BAND = KMAX * 16;                 // doubles per band
@@ -1880,6 +1883,7 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T,
     static_assert(PER >= 1 && BAND / 2 % NTH == 0, "band staging");
     __shared__ __attribute__((aligned(16))) double sC[NB][BAND];
     __shared__ int64_t next_item;
+    __shared__ int next_grp;
     __shared__ int wsum[WPB];
     const int np = (int)st->npend;
     if (np <= 0) return;
@@ -1887,14 +1891,59 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T,
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lc = lane & 15, lk = lane >> 4;
     unsigned long long touched = 0;
+    const int g0 = (int)(blockIdx.x & 7);   // blocks with the same b % 8 share an XCD
+    int gd = 0;                             // X.on: queue g0 + gd (mod 8) is being drained
     for (;;) {
         __syncthreads();
-        if (threadIdx.x == 0) next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
+        if (threadIdx.x == 0) {
+            if (X.on) {
+                int64_t it = -1;
+                int grp = 0;
+                for (; gd < 8; gd++) {
+                    grp = (g0 + gd) & 7;
+                    const int64_t cnt = flushx_group(X, grp).count;
+                    if (cnt == 0) continue;
+                    it = (int64_t)atomicAdd(&st->gwork[grp], 1ull);
+                    if (it < cnt) break;
+                    it = -1;
+                }
+                next_item = it;
+                next_grp = grp;
+            } else {
+                next_item = (int64_t)atomicAdd(&st->fwork, 1ull);
+            }
+        }
         __syncthreads();
         const int64_t item = next_item;
-        if (item >= nitems) break;
         int64_t tile, i0, i1;
-        flush_item(item, ntiles, rows, g.nloc, tile, i0, i1);
+        if (X.on) {
+            if (item < 0) break;
+            const int grp = next_grp;
+            flushx_item(X, flushx_group(X, grp), grp, item, tile, i0, i1);
+        } else {
+            if (item >= nitems) break;
+            flush_item(item, ntiles, rows, g.nloc, tile, i0, i1);
+        }
+        // region mode (launch_flush_main): a tile without block-start nonbasic
+        // columns holds live entries only in a leaving column of the block, if
+        // any (one whose trade did not move it); otherwise it is skipped
+        // without reading its pending P entries
+        if (tlive) {
+            constexpr int NCH = 32 * WPB / 64;
+            const int64_t ch = tile * NCH + threadIdx.x;
+            const bool maybe = threadIdx.x < NCH && ch < ld / 64 && tlive[ch] != 0;
+            if (!__syncthreads_or(maybe)) {
+                bool hit = false;
+                if ((int)threadIdx.x < np) {
+                    const int64_t L = lv[threadIdx.x];
+                    if (L > 0) {
+                        const int64_t p = inv[L];
+                        hit = p >= tile * (32 * WPB) && p < (tile + 1) * (32 * WPB);
+                    }
+                }
+                if (!__syncthreads_or(hit)) continue;
+            }
+        }
         const int64_t cl = tile * (32 * WPB) + wave * 32 + 2 * lc;   // this lane's column pair
         const bool in = cl < g.ncols;                                // cl even, ld even: cl + 1 < ld
         double be[G], bo[G];
@@ -2353,6 +2402,7 @@ __device__ __forceinline__ void end_block(DevState *st, const Defer &D, int kmax
         st->npend = 0;
         st->fwork = 0;
     }
+    if (q < 8) st->gwork[q] = 0;
     for (int u = q; u < kmax; u += blockDim.x) {
         D.rq[u] = kNoSlot;
         if (D.kq) D.kq[u] = 0;
@@ -2514,9 +2564,52 @@ static int64_t flush_minitems_env(int64_t def) {
     return v ? v : def;
 }
 
+static int64_t env_range(const char *name, int64_t lo, int64_t hi) {   // 0 when unset or out of range
+    const char *e = getenv(name);
+    const long long v = e ? atoll(e) : 0;
+    return (v >= lo && v <= hi) ? (int64_t)v : 0;
+}
+
+// FlushX (lpg_internal.h) for k_flushw. The band's multipliers, rs x kmax
+// doubles, are kept within a budget of that XCD's 4 MB L2 (LPG_FLUSH_CB, KB,
+// default 2048): the most column classes H whose bands fit, so P is re-read
+// by 8 / H bands (one P tile read per band: the tile's pieces run back to
+// back); bands that do not fit at H = 1 are swept in sub-bands that do. The
+// tail: two rounds of short items per group's blocks (LPG_FLUSH_XTAIL tiles).
+// xcd: -1 auto (tableaus of >= 1024 rows and >= 64 tiles), 0 off (the global
+// queue, flush_item), 1 on at any size, 10 + H on with H column classes (tests).
+static FlushX flushx_plan(int64_t ntiles, int64_t nloc, int kmax, int64_t nblocks, int xcd) {
+    FlushX X{};
+    if (xcd == 0 || nloc < 1 || ntiles < 1 || (xcd < 0 && (nloc < 1024 || ntiles < 64))) return X;
+    static const int64_t cb = env_range("LPG_FLUSH_CB", 256, 65536) * 1024;
+    static const int64_t ttf = env_range("LPG_FLUSH_XTAIL", 1, 1 << 20);
+    const int64_t budget = cb ? cb : (int64_t)2048 * 1024;
+    auto band = [&](int H) { return ((nloc + 8 / H - 1) / (8 / H) + 15) / 16 * 16; };
+    int H = 1;
+    if (xcd == 11 || xcd == 12 || xcd == 14 || xcd == 18)
+        H = xcd - 10;
+    else
+        for (int h : {8, 4, 2})
+            if (band(h) * kmax * 8 <= budget) {
+                H = h;
+                break;
+            }
+    X.ntiles = ntiles;
+    X.nloc = nloc;
+    X.H = H;
+    const int64_t rb = band(H);
+    const int64_t nsb = std::max<int64_t>(1, (rb * kmax * 8 + budget - 1) / budget);
+    X.rb = (int32_t)rb;
+    X.rs = (int32_t)std::min<int64_t>(rb, ((rb + nsb - 1) / nsb + 15) / 16 * 16);
+    X.tt = (int32_t)(ttf ? ttf : std::max<int64_t>(1, nblocks / 8 / 2));
+    X.on = 1;
+    return X;
+}
+
 // which: -1 = default (k_flushw), 0 = k_flushm (blocks of <= 32 pivots),
 // 1 = k_flushw (LPG_FLUSH_KERNEL=m|w, tests). Both bitwise.
-int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which) {
+int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &D, int kmax, int skip, int which,
+                      int xcd, const int32_t *tlive) {
     kmax = flush_kmax_supported(kmax);
     if (!kmax) return -1;
     // k_flushw by default at every block size: at 32 slots too it beats
@@ -2546,20 +2639,25 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
         if (!flush_tail_on()) rows = -rows;
         const int64_t nitems = flush_nitems(ntiles, rows, g.nloc);
         const int lb = kmax == 128 ? 1 : kmax == 96 ? 2 : kmax == 64 ? 2 : 3;   // VGPRs: 184 at 64 slots, <= 128 below
-        const int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * lb);
+        const int bmul = kmax == 64 ? 2 : 1;                                      // 8-wave blocks at 64 slots
+        const FlushX X = flushx_plan(ntiles, g.nloc, kmax, (int64_t)256 * lb / bmul, xcd);
+        int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * lb);
+        if (X.on) nblocks = (int64_t)256 * lb;
         if (nblocks < 1) return 0;
+        const unsigned grid = (unsigned)((nblocks + bmul - 1) / bmul);
+        const int32_t *TL = (tlive && D.lv && D.inv && g.ld % 64 == 0) ? tlive : nullptr;
         if (kmax == 128)
-            hipLaunchKernelGGL((k_flushw<128, 2, 1, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
-                               D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
+            hipLaunchKernelGGL((k_flushw<128, 2, 1, 4>), dim3(grid), dim3(256), 0, stream, g.T, g, st, D.Pbuf, D.Cbuf,
+                               D.cs, ntiles, nitems, rows, skip, X, TL, D.lv, D.inv);
         else if (kmax == 96)
-            hipLaunchKernelGGL((k_flushw<96, 2, 2, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
-                               D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
+            hipLaunchKernelGGL((k_flushw<96, 2, 2, 4>), dim3(grid), dim3(256), 0, stream, g.T, g, st, D.Pbuf, D.Cbuf,
+                               D.cs, ntiles, nitems, rows, skip, X, TL, D.lv, D.inv);
         else if (kmax == 64)
-            hipLaunchKernelGGL((k_flushw<64, 2, 2, kW64>), dim3((unsigned)((nblocks + 1) / 2)), dim3(64 * kW64), 0, stream,
-                               g.T, g, st, D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
+            hipLaunchKernelGGL((k_flushw<64, 2, 2, kW64>), dim3(grid), dim3(64 * kW64), 0, stream, g.T, g, st, D.Pbuf,
+                               D.Cbuf, D.cs, ntiles, nitems, rows, skip, X, TL, D.lv, D.inv);
         else
-            hipLaunchKernelGGL((k_flushw<32, 2, 3, 4>), dim3((unsigned)nblocks), dim3(256), 0, stream, g.T, g, st,
-                               D.Pbuf, D.Cbuf, D.cs, ntiles, nitems, rows, skip);
+            hipLaunchKernelGGL((k_flushw<32, 2, 3, 4>), dim3(grid), dim3(256), 0, stream, g.T, g, st, D.Pbuf, D.Cbuf,
+                               D.cs, ntiles, nitems, rows, skip, X, TL, D.lv, D.inv);
     } else {
         // k_flushm: 32-column wave tiles, 128-row strips (C tile <= 32 KB of LDS),
         // shorter strips for small tableaus; 4 blocks per CU

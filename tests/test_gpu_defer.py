@@ -174,6 +174,32 @@ def test_flush_kernels_block_sizes(lpg, monkeypatch, kernel, k, m, n, seed, kind
     _assert_same(e, o, m)
 
 
+@pytest.mark.parametrize("xcd", ["0", "1", "h1", "h2", "h4", "h8"])
+@pytest.mark.parametrize("k", [3, 32, 64, 96, 128])
+@pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1), (1100, 1300, 17, 0, 1)])
+def test_flush_item_maps_agree(lpg, monkeypatch, xcd, k, m, n, seed, kind, rule):
+    """k_flushw's global item queue (LPG_FLUSH_XCD=0) and the XCD-grouped
+    queues (FlushX: row bands x H column classes, sub-bands, short tail
+    pieces, stealing between groups) at any size and H, to optimality,
+    against the oracle. Host-side coverage of the map: tests/test_item_map.py."""
+    monkeypatch.setenv("LPG_FLUSH_KERNEL", "w")
+    monkeypatch.setenv("LPG_FLUSH_XCD", xcd)
+    e = _engine(lpg, monkeypatch, k, m, n + m + 1)
+    key = (m, n, seed, kind, rule)
+    if key not in _SOLVED:
+        o = Oracle(m, n + m + 1, nthreads=8)
+        o.generate(n, seed, kind)
+        _SOLVED[key] = (o, o.solve(200_000, rule))
+    o, ores = _SOLVED[key]
+    e.generate(n, seed, kind)
+    res = e.solve(200_000, rule)
+    assert res.status == ores.status == 1 and res.pivots == ores.pivots
+    _assert_same(e, o, m)
+
+
+_SOLVED: dict = {}
+
+
 @pytest.mark.parametrize("k", [5, 32, 40, 64, 96, 128])
 @pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1)])
 def test_generic_and_prefetching_pivot_kernels_agree(lpg, monkeypatch, k, m, n, seed, kind, rule):

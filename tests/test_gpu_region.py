@@ -227,3 +227,32 @@ def test_same_as_all_column_kernel(lpg, monkeypatch, m, n, piv, defer):
     rows = np.random.default_rng(1).choice(m, 48, replace=False)
     for i in list(rows) + [m]:
         assert np.array_equal(a.get_rows(int(i), 1), b.get_rows(int(i), 1))
+
+
+@pytest.mark.parametrize("xcd", ["0", "1", "h8"])
+@pytest.mark.parametrize("m,n,seed,kind,rule,defer", [(600, 900, 31, 0, 0, 64), (257, 300, 22, 1, 1, 96),
+                                                     (1100, 700, 33, 0, 0, 32)])
+def test_tile_liveness_map(lpg, monkeypatch, xcd, m, n, seed, kind, rule, defer):
+    """The block pass skips tiles without a block-start nonbasic column (tlive,
+    built with the region) and loads only the leaving columns' P entries on
+    the tiles they sit in: bitwise the oracle, and the pass reads and writes
+    exactly the bytes it does with the map off (LPG_FLUSH_TLIVE=0), i.e. the
+    map skips only all-zero column pairs."""
+    monkeypatch.setenv("LPG_FLUSH_XCD", xcd)
+    runs = {}
+    for tl in ("1", "0"):
+        monkeypatch.setenv("LPG_FLUSH_TLIVE", tl)
+        e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer)
+        assert e.info.region == 1
+        e.generate(n, seed, kind)
+        e.set_timing(True)
+        e.get_timing()
+        res = e.solve(200_000, rule)
+        runs[tl] = (e, res, e.get_timing().update_bytes)
+    o = Oracle(m, n + m + 1)
+    o.generate(n, seed, kind)
+    ores = o.solve(200_000, rule)
+    for tl, (e, res, _) in runs.items():
+        assert res.status == ores.status and res.pivots == ores.pivots
+        _assert_same(e, o, m)
+    assert runs["1"][2] == runs["0"][2] > 0

@@ -20,3 +20,17 @@ def test_item_map_covers_every_tile_row_once(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert out.stdout.startswith("ok ")
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_xcd_grouped_item_map_covers_every_tile_row_once(tmp_path):
+    """k_flushw's XCD-grouped map (FlushX: 8 group queues of row bands x H
+    column classes, sub-bands, short tail pieces; tests/flushx_check.cpp) over
+    shapes, H, sub-band heights and tail sizes. GPU side, bitwise:
+    tests/test_gpu_defer.py::test_flush_item_maps_agree."""
+    exe = tmp_path / "flushx_check"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "linearprogramming_amd", "csrc"),
+                    "-o", str(exe), os.path.join(ROOT, "tests", "flushx_check.cpp")], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.startswith("flushx map ok")

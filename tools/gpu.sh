@@ -17,16 +17,13 @@
 # Limits: T_PYTEST (900 s), T_BENCH (300 s), T_PY (300 s).
 # Profiles: "prof:c3:--steps 2 --warmup 0 --no-cpu", then one pmc step per
 # counter group, e.g. "pmc:fetch:FETCH_SIZE:--steps 2 --warmup 0 --no-cpu".
+# KIND@VAR=VAL,VAR2=VAL:NAME:ARGS exports those variables for that step only
+# (e.g. "pmc@LPG_FLUSH_XCD=0:fetch0:FETCH_SIZE:--steps 2 --warmup 0 --no-cpu").
 # Example: gpurun --timeout 1200 -- bash tools/gpu.sh "pytest:all:tests -m gpu -x -q" "bench:c3:--steps 20"
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for spec in "$@"; do
-    kind=${spec%%:*}
-    rest=${spec#*:}
-    name=${rest%%:*}
-    args=${rest#*:}
-    echo "[gpu.sh] $kind $name: $args" >&2
+run_step() {
     case $kind in
         pytest)
             timeout -k 10 "${T_PYTEST:-900}" python -u -m pytest $args -p no:cacheprovider --timeout 300 \
@@ -74,4 +71,15 @@ for spec in "$@"; do
             echo "unknown step kind: $kind" >&2
             exit 2 ;;
     esac
+}
+for spec in "$@"; do
+    kind=${spec%%:*}
+    rest=${spec#*:}
+    name=${rest%%:*}
+    args=${rest#*:}
+    envs=""
+    if [[ $kind == *@* ]]; then envs=${kind#*@}; kind=${kind%%@*}; fi
+    echo "[gpu.sh] $kind $name: $args ${envs:+(env $envs)}" >&2
+    ( if [ -n "$envs" ]; then IFS=',' read -ra kvs <<< "$envs"; for kv in "${kvs[@]}"; do export "$kv"; done; fi
+      run_step ) || exit $?
 done
