@@ -2017,11 +2017,27 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T,
                 d4 ae = d4{t[0].x, t[1].x, t[2].x, t[3].x};
                 d4 ao = d4{t[0].y, t[1].y, t[2].y, t[3].y};
                 const double *sa = &sC[s % NB][lk * 16 + lc];
+                // the next pair of A operands is read while this pair's four
+                // MFMAs run: left to the scheduler, every ds_read sat behind
+                // the MFMAs of the pair before and the chain waited an LDS
+                // round trip per four MFMAs (config 3, K = 96: 29.7-29.8k vs
+                // 28.6-28.8k pivots/s, profiles/r05_ab_flushw_aprefetch.log)
+                double a0 = sa[0], a1 = sa[64];
 #pragma unroll
-                for (int gq = 0; gq < G; gq++) {
-                    const double a = sa[gq * 64];
-                    ae = __builtin_amdgcn_mfma_f64_16x16x4f64(a, be[gq], ae, 0, 0, 0);
-                    ao = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bo[gq], ao, 0, 0, 0);
+                for (int gq = 0; gq < G; gq += 2) {
+                    double n0 = 0.0, n1 = 0.0;
+                    if (gq + 2 < G) {
+                        n0 = sa[(gq + 2) * 64];
+                        n1 = sa[(gq + 3) * 64];
+                    }
+                    __builtin_amdgcn_sched_barrier(0);   // the reads stay in front of the MFMAs
+                    ae = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, be[gq], ae, 0, 0, 0);
+                    ao = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bo[gq], ao, 0, 0, 0);
+                    ae = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, be[gq + 1], ae, 0, 0, 0);
+                    ao = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bo[gq + 1], ao, 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    a0 = n0;
+                    a1 = n1;
                 }
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
