@@ -20,7 +20,8 @@ sys.path.insert(0, ROOT)
 import linearprogramming_amd as lpg  # noqa: E402
 from oracle.lpo import GEN_ARTIFICIAL, GEN_DEGENERATE, GEN_DENSE, GEN_DUAL, Oracle  # noqa: E402
 
-KNOBS = ("LPG_DEFER", "LPG_PERSIST", "LPG_NO_REORDER", "LPG_FLUSH_KERNEL", "LPG_PERSIST_WG")
+KNOBS = ("LPG_DEFER", "LPG_PERSIST", "LPG_NO_REORDER", "LPG_FLUSH_KERNEL", "LPG_PERSIST_WG", "LPG_REGION",
+         "LPG_FLUSH_XCD", "LPG_FLUSH_TLIVE")
 
 
 def case(rng: random.Random, big: bool = False):
@@ -36,6 +37,9 @@ def case(rng: random.Random, big: bool = False):
         "LPG_PERSIST": rng.choice(["0", "1"]),
         "LPG_NO_REORDER": rng.choice(["0", "1"]),
         "LPG_FLUSH_KERNEL": rng.choice(["m", "w", "w"]),
+        "LPG_REGION": rng.choice(["0", "1", "1"]),
+        "LPG_FLUSH_XCD": rng.choice(["0", "1", "1", "h2", "h8"]),
+        "LPG_FLUSH_TLIVE": rng.choice(["0", "1", "1"]),
     }
     if rng.random() < 0.3:
         env["LPG_PERSIST_WG"] = str(rng.choice([8, 16, 32, 64, 128]))

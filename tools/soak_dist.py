@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 import linearprogramming_amd as lpg  # noqa: E402
 from oracle.lpo import GEN_ARTIFICIAL, GEN_DEGENERATE, GEN_DENSE, GEN_DUAL, Oracle  # noqa: E402
 
-KNOBS = ("LPG_DEFER", "LPG_PERSIST_MR", "LPG_NO_REORDER")
+KNOBS = ("LPG_DEFER", "LPG_PERSIST_MR", "LPG_NO_REORDER", "LPG_FLUSH_XCD")
 
 
 class Comm:
@@ -56,7 +56,8 @@ def case(rng):
     m = rng.choice([12, 40, 64, 100, 257, 300, 511, 700])
     n = rng.choice([16, 60, 200, 500, 1000])
     env = {"LPG_DEFER": str(rng.choice([0, 1, 3, 8, 16, 32, 33, 64, 77, 96, 128])),
-           "LPG_PERSIST_MR": rng.choice(["0", "1"]), "LPG_NO_REORDER": rng.choice(["0", "1"])}
+           "LPG_PERSIST_MR": rng.choice(["0", "1"]), "LPG_NO_REORDER": rng.choice(["0", "1"]),
+           "LPG_FLUSH_XCD": rng.choice(["0", "1", "h8"])}
     push = rng.random() < 0.6
     rule = rng.choice([0, 1]) if mode != "dual" else 0
     kind = {"primal": rng.choice([GEN_DENSE, GEN_DEGENERATE]), "two_phase": GEN_ARTIFICIAL, "big_m": GEN_ARTIFICIAL,
