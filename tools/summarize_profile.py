@@ -1,7 +1,8 @@
 """Turn the rocprofv3 output of tools/gpu.sh's prof / pmc steps into committed evidence.
 
   gpurun -- bash tools/gpu.sh "prof:rNN:ARGS" "pmc:rNN_fetch:FETCH_SIZE:ARGS" "pmc:rNN_write:WRITE_SIZE:ARGS"
-  python tools/summarize_profile.py ROUND [CONFIG]      (reads gpurun_out/prof_rNN, pmc_rNN_fetch, pmc_rNN_write)
+  python tools/summarize_profile.py ROUND [CONFIG] [TAG]   (reads gpurun_out/prof_TAG, pmc_TAG_fetch, pmc_TAG_write;
+                                                          TAG defaults to rNN)
 
 writes
   profiles/rNN_kernel_stats.csv     rocprofv3 --kernel-trace --stats summary (as produced)
@@ -52,17 +53,18 @@ def counter_means(path, counter):
 def main():
     rnd = int(sys.argv[1])
     cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    tag = sys.argv[3] if len(sys.argv) > 3 else f"r{rnd:02d}"
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    stats = _one(f"prof_r{rnd:02d}", "*kernel_stats.csv")
+    stats = _one(f"prof_{tag}", "*kernel_stats.csv")
     if stats:
-        shutil.copy(stats, os.path.join(ROOT, "profiles", f"r{rnd:02d}_kernel_stats.csv"))
+        shutil.copy(stats, os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
         with open(stats) as f:
             rows = list(csv.DictReader(f))
         for r in rows:
             print(f"{short(r['Name']):>16s} calls={r['Calls']:>6s} avg_us={float(r['AverageNs']) / 1e3:10.2f} "
                   f"pct={float(r['Percentage']):6.2f}")
-    fetch = _one(f"pmc_r{rnd:02d}_fetch", "*counter_collection.csv")
-    write = _one(f"pmc_r{rnd:02d}_write", "*counter_collection.csv")
+    fetch = _one(f"pmc_{tag}_fetch", "*counter_collection.csv")
+    write = _one(f"pmc_{tag}_write", "*counter_collection.csv")
     out = {"config": cfg, "units": "KB per dispatch (rocprofv3 FETCH_SIZE / WRITE_SIZE)",
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts half "
                          "of a 16-B/lane streaming read; MI355X_MICROARCH.md §HBM)"}
@@ -86,13 +88,13 @@ def main():
         out[f"{kern}_hbm_bytes_per_launch"] = upd
         out[f"{kern}_read_bytes"] = ff * f_kb * 1024
         out[f"{kern}_write_bytes"] = w_kb * 1024
-    with open(os.path.join(ROOT, "profiles", f"r{rnd:02d}_pmc.json"), "w") as f:
+    with open(os.path.join(ROOT, "profiles", f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
     # the stamp, shape and pending count of the build the passes measured: from
     # the bench lines those passes printed (bench.py attaches the traffic only
     # to a line with the same stamp, kernel, pending count and m / n)
     lines = []
-    for d in (f"pmc_r{rnd:02d}_fetch", f"pmc_r{rnd:02d}_write"):
+    for d in (f"pmc_{tag}_fetch", f"pmc_{tag}_write"):
         try:
             with open(os.path.join(OUT, d + ".json")) as f:
                 lines += [json.loads(x) for x in f if x.strip().startswith("{")]
@@ -103,7 +105,7 @@ def main():
     if upd is not None and len(lines) == 2 and len(stamps) == 1 and len(shapes) == 1 and None not in stamps:
         (m, n, pend), = shapes
         with open(os.path.join(ROOT, "profiles", f"pmc_config{cfg}.json"), "w") as f:
-            json.dump({"hbm_bytes_per_launch": upd, "source": f"profiles/r{rnd:02d}_pmc.json",
+            json.dump({"hbm_bytes_per_launch": upd, "source": f"profiles/{tag}_pmc.json",
                        "kernel": kern, "pending_pivots": pend, "m": m, "n": n, "source_stamp": stamps.pop(),
                        "fetch_factor": ff,
                        "how": "tools/gpu.sh pmc steps: separate rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes "
