@@ -84,3 +84,19 @@ def test_committed_files_carry_a_stamp_or_are_refused():
             m, n = bench.CONFIGS[cfg]["m"], bench.CONFIGS[cfg]["n"]
             p, why = bench.pmc_traffic(_args(cfg), rec.get("kernel"), rec.get("pending_pivots"), m, n, 1, stamp)
             assert (p is not None) == (rec.get("source_stamp") == stamp), (name, why)
+
+
+def test_roofline_names_the_binding_roofline():
+    """The pass against both rooflines: at 64 pending pivots its bytes bind
+    (HBM), at 96 its flops do (the f64 matrix cores); `achieved` / `frac` are
+    the binding one's and both are reported."""
+    touched = 8.59e9                                    # config 3: 16 B x 16384 rows x 32770 live columns
+    r64 = bench.roofline_bound(touched, 64, 1.60)
+    assert r64["bound"] == "hbm" and r64["unit"] == "GB/s"
+    assert abs(r64["achieved"] - touched / 1.60e-3 / 1e9) < 1e-6 and r64["frac"] == r64["hbm"]["frac"]
+    r96 = bench.roofline_bound(touched, 96, 2.20)
+    assert r96["bound"] == "mfma" and r96["unit"] == "TFLOP/s" and r96["peak"] == bench.MFMA_F64_PEAK_TFS
+    flops = touched / 16 * 2 * 96
+    assert abs(r96["mfma"]["algorithmic_flops_per_launch"] - flops) < 1.0
+    assert abs(r96["achieved"] - flops / 2.20e-3 / 1e12) < 1e-9 and r96["frac"] < 1.0
+    assert r96["hbm"]["unit"] == "GB/s" and abs(r96["hbm"]["achieved"] - touched / 2.20e-3 / 1e9) < 1e-6
