@@ -510,13 +510,18 @@ struct BlockArgs {
 // it stores that slot and applies its objective update at the next pivot, before
 // any reader (never priced at its own leaving pivot: d_L = -d_k P_q[L] >= 0,
 // so not eligible). Workgroup 0's thread cw + nsp holds column 0 (b).
+// On a rank of a row partition (MR): the spare of pivot sq is decided from the
+// global pivot rows of the block (rgv, D.rqg) so that every rank agrees; the
+// owner of the leaving row computes its entry as above and pushes it with its
+// pivot row's slice, the other ranks read it behind that slice's flag (bcol0 holds
+// every row of the LP, not only this rank's).
 // Preconditions kept by the host (lpg_ctx.hip region_setup): basic columns
 // are exact unit vectors with zero reduced costs, every block's column trade
 // was complete (k_swap_plan sets DevState::rbad otherwise and the launch
 // stops with kStallRegion), end_block zeroes the spares' Pbuf columns.
 template <int RULE, int NOBJ, bool MR, int KB, bool REG>
 __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
-    static_assert(!REG || (NOBJ == 1 && !MR), "region mode: one objective row, one rank");
+    static_assert(!REG || NOBJ == 1, "region mode: one objective row");
     constexpr bool B2 = KB > 64;
     constexpr int WS = B2 ? 104 : 72;                // per-wave slot rows of wm / wp
     // pricing record granules: {key, j} {P_q[phys], phys} [{dR}] [{dM}], and one
@@ -651,6 +656,11 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     }
     int64_t rqv = lane < a.q0 ? D.rq[lane] : -1;       // lane u: r_u of pending pivot u
     int64_t rqv1 = B2 && 64 + lane < a.q0 ? D.rq[64 + lane] : -1;   // bank 1: r_{64 + lane}
+    // MR + REG, lane u: the GLOBAL row of pending pivot u (rqv holds local rows,
+    // -1 off this rank): whether a spare takes over the leaving column must be
+    // decided alike on every rank
+    int64_t rgv = (MR && REG && lane < a.q0) ? D.rqg[lane] : -1;
+    int64_t rgv1 = (MR && REG && B2 && 64 + lane < a.q0) ? D.rqg[64 + lane] : -1;
     for (int u = 0; u < S; u++) {
         if (tid < cwx) sPt[u] = (u < a.q0 && hc) ? D.Pbuf[(int64_t)u * g.ld + c] : 0.0;
         if (tid < rw) sCt[u] = (u < a.q0 && hr) ? D.Cbuf[(int64_t)u * D.cs + i] : 0.0;
@@ -781,8 +791,9 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                 dR = fma(-cobl, pql, dR0);
                 st_wt(D.Pbuf + (int64_t)actq * g.ld + c, pql);
             }
-            const unsigned long long h0 = __ballot(lane < q && rqv == rs);
-            const unsigned long long h1 = B2 ? __ballot(64 + lane < q && rqv1 == rs) : 0ull;
+            // MR: this rank's candidate row, before the decision (speculative, as the pivot row)
+            const unsigned long long h0 = __ballot(lane < q && (MR ? rgv : rqv) == rs);
+            const unsigned long long h1 = B2 ? __ballot(64 + lane < q && (MR ? rgv1 : rqv1) == rs) : 0ull;
             actnow = sq == q && owns && (h0 | h1) == 0ull;
             if (actnow) bc0 = a.bcol0[rs];               // {logical, physical}: needed from the next pivot on
         }
@@ -866,6 +877,11 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                 for (int rk = 0; rk < a.X.world; rk++)
                     if (rk != a.X.rank) st_sys64(xch_row(a.X, rk, xpar, a.X.rank, g.ld) + c, v);
             }
+            if (REG && actnow) {                        // the spare's entry, at the leaving column
+                const uint64_t v = (uint64_t)__double_as_longlong(x / piv);
+                for (int rk = 0; rk < a.X.world; rk++)
+                    if (rk != a.X.rank) st_sys64(xch_row(a.X, rk, xpar, a.X.rank, g.ld) + (uint32_t)bc0, v);
+            }
             drain();
             __syncthreads();
             if (tid == 0) {
@@ -899,6 +915,17 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         }
         const bool own = !MR || (r >= g.row0 && r < g.row0 + g.nloc);   // uniform: this rank holds row r
         const int64_t rl = MR ? (own ? r - g.row0 : -1) : r;           // its local index (-1: another rank's)
+        if (MR && REG) {
+            // the decision, row r (global): a spare takes over the leaving column
+            // iff r was not pivoted earlier in the block -- on every rank alike.
+            // The owner computed its entry above (r == rs) and pushed it with its
+            // slice; the others read it behind the slice's flag below
+            const unsigned long long ga = __ballot(lane < q && rgv == r);
+            const unsigned long long gb = B2 ? __ballot(64 + lane < q && rgv1 == r) : 0ull;
+            const bool act = sq == q && (ga | gb) == 0ull;
+            if (act && !own) bc0 = a.bcol0[r];
+            actnow = act;
+        }
         if (MR && own && !(owns && r == rs)) {
             // cannot happen: the grid's minimum, if this rank holds it, is this
             // rank's minimum (unique keys). Stop loudly rather than guess.
@@ -922,6 +949,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         if (MR && wg == 0 && tid == 0) {
             st->slot[s].r = r;
             D.rq[q] = rl;
+            if (REG) D.rqg[q] = r;                      // global: later launches of the block restore rgv
             if (MR) lvv = D.basis[r];                   // stored after the P exchange: its latency hides there
             st->npend = q + 1;
             D.kq[q] = kt;
@@ -941,17 +969,21 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         }
         if (lane == q) rqv = rl;
         if (B2 && 64 + lane == q) rqv1 = rl;
+        if (MR && REG && lane == q) rgv = r;
+        if (MR && REG && B2 && 64 + lane == q) rgv1 = r;
         LPG_BPH(t, 8);
         drain();                                        // the previous phase's C stores, before this record
         LPG_BPH(t, 9);
         PricePart pb{0.0, -1, 0, 0};
         double pq = 0.0;
+        int xowner = -1;                                // MR: the rank that pushed this pivot's row
         if (own && hc) pq = x / piv;
         if (MR) {
             if (!own) {                                 // wait for this slice of P from the owner
                 // the owner: rows [floor(m p / W), floor(m (p + 1) / W)) are rank p's
                 int owner = (int)((r * (int64_t)a.X.world) / g.m);
                 while (owner + 1 < a.X.world && (g.m * (int64_t)(owner + 1)) / a.X.world <= r) owner++;
+                xowner = owner;
                 if (tid == 0) {
                     const long long t0 = (long long)wall_clock64();
                     int okx = 1;
@@ -984,7 +1016,10 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
             }
         }
         if (REG && actnow) {                           // the spare's slot q; Pbuf and d at the next pivot
-            pql = x / piv;
+            // MR, another rank's row: the owner's entry, behind the flag awaited above
+            pql = (MR && !own) ? __longlong_as_double((long long)ld_sys64(xch_row(a.X, a.X.rank, xpar, xowner, g.ld) +
+                                                                          (uint32_t)bc0))
+                               : x / piv;
             sPt[q] = pql;
             cobl = cobjR;
             actq = q;
@@ -1414,7 +1449,8 @@ __global__ __launch_bounds__(1024) void k_region_build(DevState *st, const int64
 
 // the region's preconditions on this tableau: every basic column an exact unit
 // vector (1.0 in its row, +-0 elsewhere) with a zero reduced cost; ok[0] = 0
-// on the first violation. Grid: (rows / 64, basic variables / 256).
+// on the first violation (this rank's rows: the host combines the ranks').
+// Grid: (rows / 64, basic variables / 256).
 __global__ __launch_bounds__(256) void k_region_check(const double *T, Geo g, const int64_t *basis,
                                                        const int32_t *inv, int *ok) {
     const int64_t r = (int64_t)blockIdx.y * 256 + threadIdx.x;     // basic variable of row r
@@ -1424,7 +1460,7 @@ __global__ __launch_bounds__(256) void k_region_check(const double *T, Geo g, co
     const int64_t i0 = (int64_t)blockIdx.x * 64, i1 = std::min<int64_t>(i0 + 64, g.nloc + g.nobj);
     for (int64_t i = i0; i < i1; i++) {
         const double v = T[i * g.ld + p];
-        good = good && (i < g.nloc ? v == (i == r ? 1.0 : 0.0) : v == 0.0);
+        good = good && (i < g.nloc ? v == (g.row0 + i == r ? 1.0 : 0.0) : v == 0.0);
     }
     if (!good) ok[0] = 0;
 }
@@ -1438,7 +1474,6 @@ int launch_region_build(const Launch &L, const Geo &g, DevState *st, const int64
 }
 
 int launch_region_check(const Launch &L, const Geo &g, const int64_t *basis, const int32_t *inv, int *ok) {
-    if (g.nloc != g.m) return -1;                    // one rank
     const int64_t rows = g.nloc + g.nobj;
     hipLaunchKernelGGL(k_region_check, dim3((unsigned)((rows + 63) / 64), (unsigned)((g.m + 255) / 256)), dim3(256), 0,
                        (hipStream_t)L.stream, g.T, g, basis, inv, ok);
@@ -1452,7 +1487,7 @@ int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, in
     if (n < 1 || q0 < 0 || q0 + n > ks || ks > 96 || nwg < 1 || nwg > kMaxWG || ncand < nwg || cl < 1) return -1;
     if (X && (X->world < 1 || X->world > 64 || X->nblk < nwg || X->nx < 1)) return -1;
     if (!R && ((int64_t)nwg * cw < ((g.ncols + 1) & ~(int64_t)1) || (int64_t)nwg * rw < g.nloc)) return -1;
-    if (R && (X || g.nobj != 1 || (int64_t)nwg * cw < R->nlive || (int64_t)nwg * rw < g.nloc ||
+    if (R && (g.nobj != 1 || (int64_t)nwg * cw < R->nlive || (int64_t)nwg * rw < g.nloc ||
               (int64_t)nwg * R->nsp < ks || R->cwx != cw + R->nsp + 1 || R->cwx > kNT || !R->live || !R->bcol0))
         return -1;
     if (g.nobj != 1 && g.nobj != 2) return -1;
@@ -1511,7 +1546,11 @@ int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, in
         if (X) LPG_PB_K(RU, NO, true, false); \
         else LPG_PB_K(RU, NO, false, false);  \
     } while (0)
-    if (R) {
+    if (R && X) {              // region mode on a rank of a row partition (D.rqg: global pivot rows)
+        if (!D.rqg) return -1;
+        if (rule == RULE_BLAND) LPG_PB_K(RULE_BLAND, 1, true, true);
+        else LPG_PB_K(RULE_DANTZIG, 1, true, true);
+    } else if (R) {
         if (rule == RULE_BLAND) LPG_PB_K(RULE_BLAND, 1, false, true);
         else LPG_PB_K(RULE_DANTZIG, 1, false, true);
     } else if (rule == RULE_BLAND) {

@@ -77,7 +77,7 @@ struct lpg_ctx {
     // row, the column trade, and basic columns that are exact unit vectors with
     // zero reduced costs (units_known: true after lpg_generate, or once
     // region_setup's check passed; the engine's own pivots keep it)
-    bool reg = false;             // the single-rank persistent launch runs in region mode
+    bool reg = false;             // the persistent launch runs in region mode (one rank, or every rank of a push exchange)
     bool reg_valid = false;       // live / bcol0 describe the current column order and basis
     bool units_known = false;
     RegionGeo rg{};
@@ -86,7 +86,7 @@ struct lpg_ctx {
     bool block_region = false;    // the pending block's pivots ran in region mode (its flush may use tlive)
     bool tlive_on = true;         // LPG_FLUSH_TLIVE=0: the pass reads every tile's P entries (A/B)
     int64_t *bcol0 = nullptr;
-    int *rok = nullptr;           // region_check's flag
+    int *rok = nullptr;           // region_check's flag (+ every rank's, world > 1)
     void *rec = nullptr;          // its records (zeroed once; tags never repeat within a context)
     uint32_t tag = 0;
     uint32_t pb_launch = 0;       // persistent launches since the DevState was reset (the census index)
@@ -129,6 +129,7 @@ struct lpg_ctx {
     bool permuted = false;        // colmap may differ from the identity
     int64_t cs = 0;
     int64_t *rq = nullptr;
+    int64_t *rqg = nullptr;       // region mode on ranks: the global pivot row of each pending slot
     int skip = 1;                 // column skipping in the update (LPG_FLAG_NO_SKIP turns it off)
     // the test-hook build only (LPG_TEST_HOOKS; env LPG_TEST_PENDING_FAULT=F:W):
     // before flush F, make the pending block inconsistent (W = npend | kq | lv |
@@ -326,6 +327,7 @@ static Defer defer_of(const lpg_ctx *c, int q) {
     d.Cbuf = c->Cbuf;
     d.cs = c->cs;
     d.rq = c->rq;
+    d.rqg = c->rqg;
     d.basis = c->basis;
     d.logk = c->logk;
     d.logr = c->logr;
@@ -524,18 +526,42 @@ static int cand_cap(const lpg_ctx *c) { return std::max(c->nsel, c->nsel_d); }
 // reduced cost fma(-d, 1, d) = 0). Where it fails the context leaves region
 // mode for good: the all-column slices if they fit this block size, else the
 // two-kernel pair.
+// With world > 1 (region mode on the ranks of a push exchange) the ranks
+// decide together: each checks its rows (or knows them), the flags are
+// allgathered, and region mode stays only if every rank's passed -- a rank
+// alone in region mode would run another kernel than its peers.
 static int region_setup(lpg_ctx *c) {
-    if (!c->reg || c->units_known) return 0;
-    HIPCHK(c, hipMemsetAsync(c->rok, 0xff, sizeof(int), c->stream));
-    if (launch_region_check(lau(c), geo(c), c->basis, c->inv, c->rok)) return fail(c, LPG_ERR_DEVICE, "region check failed");
-    int ok = 0;
-    HIPCHK(c, hipMemcpyAsync(&ok, c->rok, sizeof ok, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!c->reg) return 0;
+    if (c->world > 1 && !(c->persist_x && c->xmode)) return 0;   // the collectives' pair: region mode unused
+    if (c->world == 1 && c->units_known) return 0;
+    int ok = 1;
+    if (!c->units_known) {
+        HIPCHK(c, hipMemsetAsync(c->rok, 0xff, sizeof(int), c->stream));
+        if (launch_region_check(lau(c), geo(c), c->basis, c->inv, c->rok))
+            return fail(c, LPG_ERR_DEVICE, "region check failed");
+    } else {
+        HIPCHK(c, hipMemsetAsync(c->rok, 0xff, sizeof(int), c->stream));   // known: nonzero
+    }
+    if (c->world > 1) {
+        int rc = comm_allgather(c, c->rok, c->rok + 1, sizeof(int));
+        if (rc) return rc;
+        std::vector<int> all((size_t)c->world);
+        HIPCHK(c, hipMemcpyAsync(all.data(), c->rok + 1, all.size() * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        for (int v : all) ok = ok && v != 0;
+    } else {
+        HIPCHK(c, hipMemcpyAsync(&ok, c->rok, sizeof ok, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     if (ok) {
         c->units_known = true;
         return 0;
     }
     c->reg = false;
+    if (c->world > 1) {                // the all-column slices where they fit, else the pair
+        if (!c->pmr) c->persist_x = false;
+        return 0;
+    }
     if (c->pmr && !has_comm(c)) {
         c->nsel_d = c->pb_nwg;
     } else {
@@ -567,7 +593,8 @@ static int region_build(lpg_ctx *c) {
 static int enqueue_blocks(lpg_ctx *c, int64_t npiv, int rule) {
     const Geo g = geo(c);
     const bool mr = c->persist_x && c->xmode;
-    const bool reg = c->reg && !mr && !has_comm(c);
+    const bool reg = c->reg && (mr || !has_comm(c));
+    const int nwg = reg ? c->rg.nwg : c->pb_nwg;
     if (reg && !c->reg_valid) {
         int rc = region_build(c);
         if (rc) return rc;
@@ -583,8 +610,8 @@ static int enqueue_blocks(lpg_ctx *c, int64_t npiv, int rule) {
         int ncin = cand_cap(c), ncand = cand_cap(c);
         Xch X;
         if (mr) {
-            ncand = std::max(ncand, c->pb_nwg);
-            ncin = c->x_from_cand ? cand_per_rank(c) * c->world : c->pb_nwg;
+            ncand = std::max(ncand, nwg);
+            ncin = c->x_from_cand ? cand_per_rank(c) * c->world : nwg;
             if (c->x_from_cand) cin = c->cand;
             X.base = c->xbase;
             X.world = c->world;
@@ -599,8 +626,8 @@ static int enqueue_blocks(lpg_ctx *c, int64_t npiv, int rule) {
         }
         const bool ok = reg ? launch_pivot_block(lau(c), g, rule, c->st, s0, c->pend, n, c->part, ncand, cin, ncin,
                                                  c->C[s0], c->C[s1], defer_of(c, c->pend), c->rec, c->tag, c->rg.nwg,
-                                                 c->rg.cw, c->rg.rw, c->defer_k, c->rg.lds, c->pb_launch + 1, nullptr,
-                                                 0, &R) == 0
+                                                 c->rg.cw, c->rg.rw, c->defer_k, c->rg.lds, c->pb_launch + 1,
+                                                 mr ? &X : nullptr, c->xtag, &R) == 0
                             : launch_pivot_block(lau(c), g, rule, c->st, s0, c->pend, n, c->part, ncand, cin, ncin,
                                                  c->C[s0], c->C[s1], defer_of(c, c->pend), c->rec, c->tag, c->pb_nwg,
                                                  c->pb_cw, c->pb_rw, c->defer_k, c->pb_lds, c->pb_launch + 1,
@@ -999,13 +1026,13 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     // (the per-pivot work dominates: m = 2048, n = 4096 (100 MB) 100k pivots/s
     // at 32, 99k at 64; m = 4096, n = 8192 (403 MB) 77k / 82k,
     // profiles/r02_k32_64.log)
-    const int64_t nloc_guess = m * (rank + 1) / world - m * rank / world;
+    const int64_t nloc_max = (m + world - 1) / world;    // the largest row block: every rank decides alike
     // 96 once it is >= 16 GB (too big for the persistent pivot kernel's
     // slices, so the pair runs the pivots): the 96- and 128-pivot passes both
     // sit at ~47 TFLOP/s on the matrix cores (the same cost per pivot, 23%
     // below 64-pivot passes), and the pair's chains are shorter at 96 --
     // config 4: 2,424 vs 2,347 pivots/s (profiles/r03_bench_config4_k96.json)
-    const double tbytes = (double)nloc_guess * (double)ncols * 8.0;
+    const double tbytes = (double)nloc_max * (double)ncols * 8.0;
     // the block-end column trade (§3.3 of DESIGN.md) pays where the block pass
     // is long; below 2 GB on one rank its kernels cost more than scattered
     // live columns do (config 2: 105k -> 112k pivots/s without it, config 5:
@@ -1021,10 +1048,11 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
     const bool persist_ok = c->fast_pivot && !(pe && atoi(pe) == 0) && cus > 0;
-    const bool reg_ok = persist_ok && world == 1 && c->nobj == 1 && !c->no_reorder && !(pr && atoi(pr) == 0);
+    // (with world > 1 region mode runs on the ranks of a push exchange)
+    const bool reg_ok = persist_ok && c->nobj == 1 && !c->no_reorder && !(pr && atoi(pr) == 0);
     const int64_t nlive = ncols - 1 - m;                 // nonbasic columns other than column 0 (any basis)
     Geo g0{};
-    g0.nloc = nloc_guess;
+    g0.nloc = nloc_max;
     g0.nobj = c->nobj;
     g0.ncols = ncols;
     g0.m = m;
@@ -1095,12 +1123,15 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
                 c->nsel_d = c->pb_nwg;      // one ratio candidate per workgroup
             }
         }
-        // one rank: region mode where its slices fit (preferred over the all-column form)
+        // region mode where its slices fit (preferred over the all-column form);
+        // on ranks (largest row block) it runs once a push exchange is attached
         if (c->defer_k > 0 && reg_ok && nlive > 0 &&
-            block_geometry_region(g, c->defer_k, cus, pw ? atoi(pw) : 0, nlive, &c->rg) == 0) {
+            block_geometry_region(gm, c->defer_k, cus, pw ? atoi(pw) : 0, nlive, &c->rg) == 0) {
             c->reg = true;
-            c->persist = true;
-            c->nsel_d = c->rg.nwg;
+            if (world == 1) {
+                c->persist = true;
+                c->nsel_d = c->rg.nwg;
+            }
         }
     }
 #define ALLOC(p, bytes)                                                                    \
@@ -1130,7 +1161,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         ALLOC(c->mark, (size_t)c->ld * sizeof(int32_t));
         ALLOC(c->tlive, (size_t)(c->ld / 64 + 1) * sizeof(int32_t));
         ALLOC(c->bcol0, (size_t)m * sizeof(int64_t));
-        ALLOC(c->rok, sizeof(int));
+        ALLOC(c->rok, (size_t)(1 + world) * sizeof(int));
     }
     if (world > 1) ALLOC(c->cand, (size_t)std::max(c->nsel, c->nsel_d) * world * sizeof(Cand));
     else c->cand = c->part;
@@ -1143,6 +1174,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         ALLOC(c->Pbuf, (size_t)slots * c->ld * sizeof(double));
         ALLOC(c->Cbuf, (size_t)slots * c->cs * sizeof(double));
         ALLOC(c->rq, (size_t)slots * sizeof(int64_t));
+        if (c->reg) ALLOC(c->rqg, (size_t)slots * sizeof(int64_t));
         ALLOC(c->zrow, (size_t)c->ld * sizeof(double));
         ALLOC(c->kq, (size_t)slots * sizeof(int64_t));
         ALLOC(c->lv, (size_t)slots * sizeof(int64_t));
@@ -1251,7 +1283,8 @@ int lpg_comm_init_host(lpg_ctx *c, const lpg_host_comm_ops *ops) {
 static int ensure_xbuf(lpg_ctx *c) {
     if (c->xbuf) return 0;
     if (!(c->defer_k > 0 && c->fast_pivot)) return fail(c, LPG_ERR_STATE, "push exchange needs the deferred pivot pair");
-    c->xnblk = std::max(c->npp_d, c->pmr ? c->pb_nwg : 0);   // P chunk flags: prep blocks / k_pivot_block slices
+    // P chunk flags: prep blocks / k_pivot_block slices (all-column or region)
+    c->xnblk = std::max({c->npp_d, c->pmr ? c->pb_nwg : 0, c->reg ? c->rg.nwg : 0});
     c->xnx = c->nsel_d;
     c->xbytes = xch_bytes(c->ld, c->world, c->xnblk, c->xnx, &c->xoffF, &c->xoffC, &c->xoffG);
     // uncached: a peer's stores over xGMI land in this GPU's HBM behind its
@@ -1322,7 +1355,7 @@ static int attach_push(lpg_ctx *c, std::vector<char *> &bases) {
     // the pivot loop as one launch per block on every rank (LPG_PERSIST=0 or
     // LPG_PERSIST_MR=0: the two-kernel pair)
     const char *pe = getenv("LPG_PERSIST"), *pm = getenv("LPG_PERSIST_MR");
-    c->persist_x = c->pmr && !(pe && atoi(pe) == 0) && !(pm && atoi(pm) == 0);
+    c->persist_x = (c->pmr || c->reg) && !(pe && atoi(pe) == 0) && !(pm && atoi(pm) == 0);
     return 0;
 }
 
@@ -1402,7 +1435,7 @@ void lpg_destroy(lpg_ctx *c) {
     for (hipEvent_t e : c->tr.ev) (void)hipEventDestroy(e);
     if (c->cand && c->cand != c->part) (void)hipFree(c->cand);
     void *bufs[] = {c->T, c->P, c->C[0], c->C[1], c->acc, c->cb, c->cost, c->pp, c->pc, c->part, c->basis, c->logk, c->logr, c->st,
-                    c->Pbuf, c->Cbuf, c->rq, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->mul, c->pv, c->tmp,
+                    c->Pbuf, c->Cbuf, c->rq, c->rqg, c->zrow, c->kq, c->lv, c->colmap, c->inv, c->pairs, c->mul, c->pv, c->tmp,
                     c->rec, c->drc, c->dcp, c->drc_all, c->live, c->mark, c->bcol0, c->rok, c->tlive};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -1422,12 +1455,13 @@ int lpg_info(const lpg_ctx *c, lpg_info_t *o) {
     o->device = c->device;
     o->nobj = (int32_t)c->nobj;
     o->defer_k = c->defer_k;
-    o->pivot_wg = (c->persist && !has_comm(c)) ? (c->reg ? c->rg.nwg : c->pb_nwg) : ((c->persist_x && c->xmode) ? c->pb_nwg : 0);
+    const bool pb = (c->persist && !has_comm(c)) || (c->persist_x && c->xmode);
+    o->pivot_wg = pb ? (c->reg ? c->rg.nwg : c->pb_nwg) : 0;
     o->bytes_per_pivot = 16.0 * (double)(c->nloc + c->nobj) * (double)c->ncols;
     o->exchange = c->xmode ? (c->xuncached ? 2 : 1) : 0;
     o->column_trade = reorders(c) ? 1 : 0;
     o->residency_fallbacks = c->res_fallbacks;
-    o->region = (o->pivot_wg > 0 && c->reg && !has_comm(c)) ? 1 : 0;
+    o->region = (o->pivot_wg > 0 && c->reg) ? 1 : 0;
     return 0;
 }
 

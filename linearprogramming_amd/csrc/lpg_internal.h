@@ -76,6 +76,7 @@ struct Defer {
     double  *Cbuf;            // K x cs: C_q (column-major per pivot, rows 0..nloc-1)
     int64_t  cs;              // Cbuf pitch (>= nloc)
     int64_t *rq;              // K: local pivot row of pivot q, -1 on a non-owner rank
+    int64_t *rqg;             // K: global pivot row of pivot q (region mode on a rank of a partition), or null
     int64_t *basis, *logk, *logr;   // bookkeeping done by prep_t in deferred mode
     const double *zrow;       // ld zeros (the padding slots of the prefetching pivot kernels)
     int64_t *kq, *lv;         // K: entering / leaving variable of pending pivot q (logical; k_swap_plan)

@@ -2431,13 +2431,14 @@ __global__ __launch_bounds__(kBlock) void k_end_block(DevState *__restrict__ st,
 }
 
 // bcol0 (region mode): every row's basic column for the next block, {logical, physical}
+// (all m rows of the LP: on a rank of a row partition the spare of a pivot on
+// another rank's row reads it too)
 __global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Geo g, const int32_t *__restrict__ pairs,
                                                       DevState *__restrict__ st, Defer D, int kmax,
                                                       int64_t *__restrict__ bcol0) {
     if (st && blockIdx.x == 0 && blockIdx.y == 0) end_block(st, D, kmax, bcol0 != nullptr, g.ld);
     if (bcol0 && blockIdx.y == 0) {
-        const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-        if (r < g.m) {
+        for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < g.m; r += (int64_t)gridDim.x * kBlock) {
             const int64_t v = D.basis[r];
             bcol0[r] = (v << 32) | (int64_t)(uint32_t)D.inv[v];
         }
@@ -2470,7 +2471,7 @@ int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const De
 int launch_fill_cols(const Launch &L, const Geo &g, const int32_t *pairs, DevState *st, const Defer *D, int kmax,
                      int64_t *bcol0) {
     if (st && (!D || !D->rq || kmax < 1 || kmax > LPG_DEFER_MAX)) return -1;
-    if (bcol0 && (!st || g.nloc != g.m || !D->basis || !D->inv || !D->lv || !D->Pbuf)) return -1;   // region: one rank
+    if (bcol0 && (!st || !D->basis || !D->inv || !D->lv || !D->Pbuf)) return -1;
     hipLaunchKernelGGL(k_fill_cols, dim3((unsigned)std::max<int64_t>((g.nloc + kBlock - 1) / kBlock, 1), 4), dim3(kBlock),
                        0, (hipStream_t)L.stream, g.T, g, pairs, st, D ? *D : Defer{}, kmax, bcol0);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -148,7 +148,9 @@ def test_threads_row_partition_bitwise(lpg, world, m, n, kind, rule, defer, monk
 
 
 def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule=0, defer=None, mr=None, big_m=False,
-                 two_phase=False, dual=False):
+                 two_phase=False, dual=False, region=None):
+    if region is not None:                        # 0: the all-column slices instead of region mode
+        os.environ["LPG_REGION"] = region
     if defer is not None:
         os.environ["LPG_DEFER"] = defer
     if mr is not None:                            # 0: the two-kernel pair instead of k_pivot_block's multi-rank form
@@ -196,19 +198,22 @@ def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule
     info = e.info
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump(dict(status=res.status, pivots=res.pivots, log=e.get_log(), basis=e.get_basis(), wg=info.pivot_wg,
+                         region=info.region,
                          rows=e.get_rows(info.row0, info.nrows), obj=e.get_rows(m, 2 if big_m else 1)), f)
     e.close()
     dist.destroy_process_group()
 
 
-def _processes(world, m, n, seed, push, kind=0, rule=0, defer=None, mr=None, big_m=False, two_phase=False, dual=False):
+def _processes(world, m, n, seed, push, kind=0, rule=0, defer=None, mr=None, big_m=False, two_phase=False, dual=False,
+               region=None):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_gloo_worker, args=(world, port, m, n, seed, d, push, kind, rule, defer, mr, big_m, two_phase, dual),
+        mp.spawn(_gloo_worker, args=(world, port, m, n, seed, d, push, kind, rule, defer, mr, big_m, two_phase, dual,
+                                     region),
                  nprocs=world, join=True)
         parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     if big_m:
@@ -283,12 +288,12 @@ def test_processes_dual_bitwise(lpg, world, m, n, seed, defer):
     _processes(world, m, n, seed, push=world == 2, defer=defer, dual=True)   # the push attached: unused, harmless
 
 
-@pytest.mark.parametrize("mr", [None, "0"])
+@pytest.mark.parametrize("mr,region", [(None, None), (None, "0"), ("0", None)])
 @pytest.mark.parametrize("world,m,n,kind,rule,defer", [(2, 120, 200, 0, 0, None), (2, 96, 160, 0, 0, "5"),
                                                        (3, 101, 77, 0, 0, "64"), (2, 64, 64, 1, 1, "5"),
                                                        (3, 203, 301, 0, 0, "32"), (2, 203, 301, 0, 0, "128"),
                                                        (2, 1024, 2048, 0, 0, None), (3, 700, 900, 1, 1, "64")])
-def test_processes_owner_push_bitwise(lpg, world, m, n, kind, rule, defer, mr):
+def test_processes_owner_push_bitwise(lpg, world, m, n, kind, rule, defer, mr, region):
     """The owner-push exchange between ranks in separate processes sharing the
     GPU (IPC-mapped exchange buffers, the layout of one process per GPU): no
     collective per pivot -- the owner stores the pivot row into every rank's
@@ -299,10 +304,15 @@ def test_processes_owner_push_bitwise(lpg, world, m, n, kind, rule, defer, mr):
     By default (mr None) every rank runs k_pivot_block's multi-rank form --
     one launch per block, the leaving row and the pivot row exchanged inside
     it -- wherever its slices fit (blocks of <= 64 pivots); mr "0" keeps the
-    two-kernel pair."""
-    parts = _processes(world, m, n, 778, push=True, kind=kind, rule=rule, defer=defer, mr=mr)
+    two-kernel pair. Round 5: that launch runs in region mode on every rank
+    (slices of the live columns only, a spare per pending pivot taking over
+    its leaving column, decided from the global pivot rows so every rank
+    agrees; a non-owner reads the spare's entry from the owner's push);
+    region "0" keeps the all-column slices."""
+    parts = _processes(world, m, n, 778, push=True, kind=kind, rule=rule, defer=defer, mr=mr, region=region)
     persistent = mr is None and (defer is None or int(defer) <= 64)
     assert all((p["wg"] > 0) == persistent for p in parts)
+    assert all(p["region"] == (persistent and region is None) for p in parts)
     assert len({p["wg"] for p in parts}) == 1          # the same slices on every rank
 
 
@@ -322,6 +332,7 @@ def test_processes_4_ranks(lpg, world, m, n, kind, rule, defer, push, mr):
     no GPU between ranks."""
     parts = _processes(world, m, n, 778, push=push, kind=kind, rule=rule, defer=defer, mr=mr)
     assert all((p["wg"] > 0) == (push and mr is None) for p in parts)
+    assert all(p["region"] == (push and mr is None) for p in parts)
     assert len({p["wg"] for p in parts}) == 1
 
 
@@ -390,19 +401,25 @@ def test_host_comm_single_rank(lpg):
         e.comm_init_host(lambda b: b, lambda a: a)     # one communicator per context
 
 
+@pytest.mark.parametrize("trade", [None, "1"])
 @pytest.mark.parametrize("mr", ["1", "0"])
 @pytest.mark.parametrize("m,n", [(300, 500), (1024, 2048)])
-def test_owner_push_single_rank(lpg, m, n, mr, monkeypatch):
+def test_owner_push_single_rank(lpg, m, n, mr, trade, monkeypatch):
     """The owner-push exchange on a 1-rank communicator (pushes to itself):
     k_pivot_block's multi-rank form (mr 1) and the two-kernel pair (mr 0),
-    bitwise the engine without a communicator and the oracle."""
+    bitwise the engine without a communicator and the oracle. trade "1": the
+    block-end column trade on (one rank below 2 GB keeps it off by default),
+    with it region mode on the multi-rank form."""
     monkeypatch.setenv("LPG_DEFER", "64")
     monkeypatch.setenv("LPG_PERSIST_MR", mr)
+    if trade is not None:
+        monkeypatch.setenv("LPG_NO_REORDER", "0")
     e = lpg.Engine(m, n + m + 1)
     e.comm_init_host(lambda b: b, lambda a: a)
     e.comm_init_push([e.push_handle()])
     assert e.info.exchange in (1, 2)                # 2: the exchange buffer is uncached (hipDeviceMallocUncached)
     assert (e.info.pivot_wg > 0) == (mr == "1")
+    assert e.info.region == (mr == "1" and trade == "1")   # region mode on the ranks of a push exchange (round 5)
     print(f"exchange mode {e.info.exchange}")
     e.generate(n, 43, 0)
     res = e.solve(100_000, 0)
