@@ -1061,9 +1061,12 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     // region's slices hold 96 slots: the 96-pivot pass costs ~12% less per
     // pivot than the 64-pivot one (config-3 shape: 2.15 vs 1.625 ms per pass,
     // profiles/r04_flush96_lab.log, r04_ab_k72_*), which the all-column
-    // slices could not hold (config 3: 49,153 columns at 96 slots = 37 MB of LDS)
+    // slices could not hold (config 3: 49,153 columns at 96 slots = 37 MB of LDS).
+    // On the ranks of a row partition from 1 GB: config 3's P = 4 rank (4096
+    // rows, stand-in with the push and the trade) 48.8k pivots/s at 64, 54.6k
+    // at 96; P = 8 (0.8 GB) 60.8k vs 59.5k (profiles/r05_ab_mrreg_p48.log)
     RegionGeo rg96{};
-    if (reg_ok && tbytes >= 2e9 && tbytes < 16e9 && nlive > 0 &&
+    if (reg_ok && tbytes >= (world > 1 ? 1e9 : 2e9) && tbytes < 16e9 && nlive > 0 &&
         block_geometry_region(g0, 96, cus, pw ? atoi(pw) : 0, nlive, &rg96) == 0)
         kdef = 96;
     c->defer_k = (flags & LPG_FLAG_EAGER) ? 0 : (dk ? atoi(dk) : kdef);

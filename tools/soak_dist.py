@@ -7,6 +7,12 @@ basis, objective row(s) and its own constraint rows with the oracle
 (np.array_equal). Exits 1 on the first mismatch.
 
     python tools/soak_dist.py [seconds] [seed]
+
+With LPG_PUSH_SHARED_QUEUES=1 in the environment the owner push runs between
+the rank threads (the multi-rank pivot launch, in region mode where LPG_REGION
+allows and the column trade is on); exchange timeouts are then counted, not
+compared (threads share the process's hardware queues). SOAK_DIST_FOCUS=region
+draws only cases of that launch in region mode.
 """
 import os
 import random
@@ -21,7 +27,7 @@ sys.path.insert(0, ROOT)
 import linearprogramming_amd as lpg  # noqa: E402
 from oracle.lpo import GEN_ARTIFICIAL, GEN_DEGENERATE, GEN_DENSE, GEN_DUAL, Oracle  # noqa: E402
 
-KNOBS = ("LPG_DEFER", "LPG_PERSIST_MR", "LPG_NO_REORDER", "LPG_FLUSH_XCD")
+KNOBS = ("LPG_DEFER", "LPG_PERSIST_MR", "LPG_NO_REORDER", "LPG_FLUSH_XCD", "LPG_REGION")
 
 
 class Comm:
@@ -57,8 +63,13 @@ def case(rng):
     n = rng.choice([16, 60, 200, 500, 1000])
     env = {"LPG_DEFER": str(rng.choice([0, 1, 3, 8, 16, 32, 33, 64, 77, 96, 128])),
            "LPG_PERSIST_MR": rng.choice(["0", "1"]), "LPG_NO_REORDER": rng.choice(["0", "1"]),
-           "LPG_FLUSH_XCD": rng.choice(["0", "1", "h8"])}
+           "LPG_FLUSH_XCD": rng.choice(["0", "1", "h8"]), "LPG_REGION": rng.choice(["0", "1", "1"])}
     push = rng.random() < 0.6
+    if os.environ.get("SOAK_DIST_FOCUS") == "region":   # the multi-rank launch in region mode only
+        env.update({"LPG_DEFER": str(rng.choice([3, 8, 16, 32, 33, 64, 77, 96])), "LPG_PERSIST_MR": "1",
+                    "LPG_NO_REORDER": "0", "LPG_REGION": "1"})
+        mode = rng.choice(["primal", "primal", "two_phase"])
+        push = True
     rule = rng.choice([0, 1]) if mode != "dual" else 0
     kind = {"primal": rng.choice([GEN_DENSE, GEN_DEGENERATE]), "two_phase": GEN_ARTIFICIAL, "big_m": GEN_ARTIFICIAL,
             "dual": GEN_DUAL}[mode]
