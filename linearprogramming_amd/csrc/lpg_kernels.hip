@@ -1879,8 +1879,9 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T,
     constexpr int NTH = 64 * WPB;
     constexpr int G = KMAX / 4;
     constexpr int BAND = KMAX * 16;                 // doubles per band
-    constexpr int PER = BAND / 2 / NTH;             // 16-byte multiplier pieces per thread per band
-    static_assert(PER >= 1 && BAND / 2 % NTH == 0, "band staging");
+    constexpr int NPC = BAND / 2;                   // 16-byte multiplier pieces per band
+    constexpr int PER = (NPC + NTH - 1) / NTH;      // ... per thread (the last round partial when NTH does not divide)
+    static_assert(PER >= 1, "band staging");
     __shared__ __attribute__((aligned(16))) double sC[NB][BAND];
     __shared__ int64_t next_item;
     __shared__ int next_grp;
@@ -1983,13 +1984,15 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw(double *__restrict__ T,
                 const int q = e >> 3, rr = 2 * (e & 7);
                 const int64_t row = i0 + 16 * s + rr;
                 d2 v = d2{0.0, 0.0};
-                if (s < nb && q < np && row < i1) v = *(const d2 *)(Cbuf + (int64_t)q * cs + row);   // row + 1 < cs
+                if (s < nb && q < np && row < i1 && (NPC % NTH == 0 || e < NPC))
+                    v = *(const d2 *)(Cbuf + (int64_t)q * cs + row);   // row + 1 < cs
                 cr[u] = -v;
             }
         };
         auto cstore = [&](const d2 (&cr)[PER], int s) {
 #pragma unroll
-            for (int u = 0; u < PER; u++) *(d2 *)(&sC[s % NB][2 * (threadIdx.x + u * NTH)]) = cr[u];
+            for (int u = 0; u < PER; u++)
+                if (NPC % NTH == 0 || threadIdx.x + u * NTH < NPC) *(d2 *)(&sC[s % NB][2 * (threadIdx.x + u * NTH)]) = cr[u];
         };
         for (int s = 0; s < NB - 1; s++) {   // prologue: bands 0 .. NB-2 into the ring
             d2 cr[PER];
@@ -2642,7 +2645,13 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
         // per 8 waves instead of 4; config 3: 25.25k vs 25.04k pivots/s,
         // interleaved A/B, profiles/r03_ab_flushw_wpb8.log)
         constexpr int kW64 = 8;
-        const int tw = kmax == 64 ? 32 * kW64 : 128;   // tile width: 32 columns per wave
+        // 96 slots: 8-wave blocks too (2 KB per tableau row per block instead of
+        // 1 KB, one multiplier band staged for 8 waves): pass 2.177 -> 2.144 ms at
+        // config 3, 35.23 -> 34.73 ms at config 4, three interleaved pairs
+        // (profiles/r05_ab_flushw_w8.log); LPG_FLUSH_W96=4 restores 4-wave blocks
+        static const int w96 = env_range("LPG_FLUSH_W96", 4, 4) == 4 ? 4 : 8;
+        const bool wide = kmax == 64 || (kmax == 96 && w96 == 8);
+        const int tw = wide ? 32 * kW64 : 128;   // tile width: 32 columns per wave
         const int64_t ntiles = (g.ncols + tw - 1) / tw;
         // Items of up to 2048 rows (round 4, with the short tail items): config 4
         // pass 34.5 -> 33.5 ms per 96-pivot block at 2048 vs 512 rows, 4096 /
@@ -2656,7 +2665,7 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
         if (!flush_tail_on()) rows = -rows;
         const int64_t nitems = flush_nitems(ntiles, rows, g.nloc);
         const int lb = kmax == 128 ? 1 : kmax == 96 ? 2 : kmax == 64 ? 2 : 3;   // VGPRs: 184 at 64 slots, <= 128 below
-        const int bmul = kmax == 64 ? 2 : 1;                                      // 8-wave blocks at 64 slots
+        const int bmul = wide ? 2 : 1;                                            // 8-wave blocks at 64 slots
         const FlushX X = flushx_plan(ntiles, g.nloc, kmax, (int64_t)256 * lb / bmul, xcd);
         int64_t nblocks = std::min<int64_t>(nitems, (int64_t)256 * lb);
         if (X.on) nblocks = (int64_t)256 * lb;
@@ -2665,6 +2674,9 @@ int launch_flush_main(const Launch &L, const Geo &g, DevState *st, const Defer &
         const int32_t *TL = (tlive && D.lv && D.inv && g.ld % 64 == 0) ? tlive : nullptr;
         if (kmax == 128)
             hipLaunchKernelGGL((k_flushw<128, 2, 1, 4>), dim3(grid), dim3(256), 0, stream, g.T, g, st, D.Pbuf, D.Cbuf,
+                               D.cs, ntiles, nitems, rows, skip, X, TL, D.lv, D.inv);
+        else if (kmax == 96 && wide)
+            hipLaunchKernelGGL((k_flushw<96, 2, 1, 8>), dim3(grid), dim3(512), 0, stream, g.T, g, st, D.Pbuf, D.Cbuf,
                                D.cs, ntiles, nitems, rows, skip, X, TL, D.lv, D.inv);
         else if (kmax == 96)
             hipLaunchKernelGGL((k_flushw<96, 2, 2, 4>), dim3(grid), dim3(256), 0, stream, g.T, g, st, D.Pbuf, D.Cbuf,
