@@ -1448,7 +1448,7 @@ __global__ __launch_bounds__(1024) void k_region_build(DevState *st, const int64
 }
 
 // the region's preconditions on this tableau: every basic column an exact unit
-// vector (1.0 in its row, +-0 elsewhere) with a zero reduced cost; ok[0] = 0
+// vector (1.0 in its row, +0 elsewhere) with a zero reduced cost; ok[0] = 0
 // on the first violation (this rank's rows: the host combines the ranks').
 // Grid: (rows / 64, basic variables / 256).
 __global__ __launch_bounds__(256) void k_region_check(const double *T, Geo g, const int64_t *basis,
@@ -1460,7 +1460,9 @@ __global__ __launch_bounds__(256) void k_region_check(const double *T, Geo g, co
     const int64_t i0 = (int64_t)blockIdx.x * 64, i1 = std::min<int64_t>(i0 + 64, g.nloc + g.nobj);
     for (int64_t i = i0; i < i1; i++) {
         const double v = T[i * g.ld + p];
-        good = good && (i < g.nloc ? v == (g.row0 + i == r ? 1.0 : 0.0) : v == 0.0);
+        // bit for bit (+0, not -0: k_move_cols writes a leaving column's base data as +0 / 1.0)
+        const uint64_t want = g.row0 + i == r ? 0x3ff0000000000000ull : 0ull;
+        good = good && (i < g.nloc ? (uint64_t)__double_as_longlong(v) == want : v == 0.0);
     }
     if (!good) ok[0] = 0;
 }

@@ -85,6 +85,7 @@ struct lpg_ctx {
     int32_t *tlive = nullptr;     // region: 64-column chunks holding a block-start nonbasic column (k_flushw skips the rest)
     bool block_region = false;    // the pending block's pivots ran in region mode (its flush may use tlive)
     bool tlive_on = true;         // LPG_FLUSH_TLIVE=0: the pass reads every tile's P entries (A/B)
+    bool move_unit = true;        // LPG_MOVE_UNIT=0: k_move_cols reads the leaving columns (A/B)
     int64_t *bcol0 = nullptr;
     int *rok = nullptr;           // region_check's flag (+ every rank's, world > 1)
     void *rec = nullptr;          // its records (zeroed once; tags never repeat within a context)
@@ -388,8 +389,12 @@ static int flush_launch(lpg_ctx *c) {
     if (c->inject_flush >= 0 && c->nflush == c->inject_flush && (rc = inject_pending_fault(c))) return rc;
 #endif
     c->nflush++;
+    // unit: the leaving columns' base data is their unit vector (a region block:
+    // the basic columns were checked exact unit vectors, and the trade, the
+    // pass and k_fill_cols keep them so), written without reading it
+    const int unit = (c->block_region && c->reg_valid && c->move_unit) ? 1 : 0;
     if (launch_swap_plan(lau(c), geo(c), c->st, defer_of(c, 0), c->colmap, c->inv, c->pairs, re ? 1 : 0, c->defer_k) ||
-        (re && launch_move_cols(lau(c), geo(c), c->st, defer_of(c, 0), c->pairs)))
+        (re && launch_move_cols(lau(c), geo(c), c->st, defer_of(c, 0), c->pairs, unit)))
         return fail(c, LPG_ERR_DEVICE, "swap plan launch failed");
     if (c->timing && ((rc = timing_mark(c, 0)) || (rc = timing_mark(c, 1)))) return rc;
     // tlive: region blocks only (every pivot recorded its leaving column, the
@@ -1096,6 +1101,10 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
     // latter with H column classes (tests, A/B); unset: by size
     const char *ft = getenv("LPG_FLUSH_TLIVE");
     c->tlive_on = !(ft && ft[0] == '0');
+    {
+        const char *mu = getenv("LPG_MOVE_UNIT");
+        c->move_unit = !(mu && mu[0] == '0');
+    }
     const char *fx = getenv("LPG_FLUSH_XCD");
     c->flush_xcd = -1;
     if (fx && fx[0] == '0') c->flush_xcd = 0;
@@ -1183,7 +1192,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
         ALLOC(c->lv, (size_t)slots * sizeof(int64_t));
         ALLOC(c->colmap, (size_t)c->ld * sizeof(int32_t));
         ALLOC(c->inv, (size_t)c->ld * sizeof(int32_t));
-        ALLOC(c->pairs, (size_t)(1 + 3 * LPG_DEFER_MAX) * sizeof(int32_t));
+        ALLOC(c->pairs, (size_t)(1 + kPairW * LPG_DEFER_MAX) * sizeof(int32_t));
         ALLOC(c->mul, (size_t)LPG_DEFER_MAX * LPG_DEFER_MAX * sizeof(double));
         ALLOC(c->pv, (size_t)slots * sizeof(double));
     }

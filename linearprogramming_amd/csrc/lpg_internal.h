@@ -360,7 +360,13 @@ int flush_kmax_supported(int k);     // smallest compiled pending bound >= k (0:
 // out of range, stops the loop with kStallPending instead of indexing).
 int launch_swap_plan(const Launch &L, const Geo &g, DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
                      int32_t *pairs, int plan, int kmax);   // reads D.pv (replicated pivot elements)
-int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs);
+// pairs: count, then kPairW ints per pair {E's position a, L's position b,
+// E's row, L's row at the block start (-1: another rank's)}. unit: L's base
+// column is known to be its unit vector (region mode checked it), so the
+// constraint rows write it without reading it.
+constexpr int kPairW = 4;
+int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs,
+                     int unit);
 // st != nullptr: also ends the pending block (npend, fwork, and D's kmax slots
 // back to their never-filled sentinels), in place of launch_flush_tail's
 // k_end_block (one dispatch fewer per block)

@@ -2321,19 +2321,23 @@ __global__ __launch_bounds__(kPlanNT) void k_swap_plan(DevState *__restrict__ st
     }
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int ie = oE + __popcll(me & below), il = oL + __popcll(ml & below);
-    __shared__ int64_t eE[kPlanNT], eL[kPlanNT], eR[kPlanNT];
+    __shared__ int64_t eE[kPlanNT], eL[kPlanNT], eR[kPlanNT], eRL[kPlanNT];
     if (inE) {
         eE[ie] = x;
         eR[ie] = rx;
     }
-    if (inL) eL[il] = y;
+    if (inL) {
+        eL[il] = y;
+        eRL[il] = rx;      // y was basic in row r_q from the block start until it left at q
+    }
     __syncthreads();
     if (q < n) {
         const int64_t ce = eE[q], cl = eL[q];
         const int32_t a = inv[ce], b = inv[cl];
-        pairs[1 + 3 * q] = a;
-        pairs[2 + 3 * q] = b;
-        pairs[3 + 3 * q] = (int32_t)eR[q];
+        pairs[1 + kPairW * q] = a;
+        pairs[2 + kPairW * q] = b;
+        pairs[3 + kPairW * q] = (int32_t)eR[q];
+        pairs[4 + kPairW * q] = (int32_t)eRL[q];
         colmap[a] = (int32_t)cl;
         colmap[b] = (int32_t)ce;
         inv[cl] = a;
@@ -2349,7 +2353,7 @@ __global__ __launch_bounds__(kPlanNT) void k_swap_plan(DevState *__restrict__ st
 // loads took ~40 us to make).
 __global__ __launch_bounds__(kBlock) void k_move_cols(double *__restrict__ T, Geo g, const DevState *__restrict__ st,
                                                       double *__restrict__ Pbuf, const int32_t *__restrict__ pairs,
-                                                      int npb) {
+                                                      int npb, int unit) {
     const int n = pairs[0];
     if (n == 0) return;
     const int nrb = (int)gridDim.x - npb;
@@ -2360,7 +2364,7 @@ __global__ __launch_bounds__(kBlock) void k_move_cols(double *__restrict__ T, Ge
              e += nt) {
             const int q = e / n, p = e - q * n;
             double *Pq = Pbuf + (int64_t)q * g.ld;
-            const int32_t a = pairs[1 + 3 * p], b = pairs[2 + 3 * p];
+            const int32_t a = pairs[1 + kPairW * p], b = pairs[2 + kPairW * p];
             Pq[a] = Pq[b];
             Pq[b] = 0.0;
         }
@@ -2372,15 +2376,18 @@ __global__ __launch_bounds__(kBlock) void k_move_cols(double *__restrict__ T, Ge
     double *row = T + i * g.ld;
     for (int p0 = 16 * blockIdx.y; p0 < n; p0 += 16 * gridDim.y) {      // 16 pairs' loads in flight at once
         double va[16], vb[16];
-        int ia[16], ib[16];
+        int ia[16], ib[16], rl[16];
 #pragma unroll
         for (int u = 0; u < 16; u++) {
-            ia[u] = p0 + u < n ? pairs[1 + 3 * (p0 + u)] : 0;
-            ib[u] = p0 + u < n ? pairs[2 + 3 * (p0 + u)] : 0;
+            ia[u] = p0 + u < n ? pairs[1 + kPairW * (p0 + u)] : 0;
+            ib[u] = p0 + u < n ? pairs[2 + kPairW * (p0 + u)] : 0;
+            rl[u] = p0 + u < n ? pairs[4 + kPairW * (p0 + u)] : -1;
         }
+        // unit: L's base column is the unit vector of its row (-1: another
+        // rank's), so a constraint row writes it without reading it
 #pragma unroll
         for (int u = 0; u < 16; u++) {
-            vb[u] = row[ib[u]];
+            vb[u] = (unit && !obj) ? ((int64_t)rl[u] == i ? 1.0 : 0.0) : row[ib[u]];
             va[u] = obj ? row[ia[u]] : 0.0;
         }
 #pragma unroll
@@ -2451,7 +2458,7 @@ __global__ __launch_bounds__(kBlock) void k_fill_cols(double *__restrict__ T, Ge
     if (i >= g.nloc || n == 0) return;
     double *row = T + i * g.ld;
     for (int p = blockIdx.y; p < n; p += gridDim.y)
-        row[pairs[2 + 3 * p]] = (i == (int64_t)pairs[3 + 3 * p]) ? 1.0 : 0.0;
+        row[pairs[2 + kPairW * p]] = (i == (int64_t)pairs[3 + kPairW * p]) ? 1.0 : 0.0;
 }
 
 int launch_swap_plan(const Launch &L, const Geo &g, DevState *st, const Defer &D, int32_t *colmap, int32_t *inv,
@@ -2463,11 +2470,12 @@ int launch_swap_plan(const Launch &L, const Geo &g, DevState *st, const Defer &D
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs) {
+int launch_move_cols(const Launch &L, const Geo &g, const DevState *st, const Defer &D, const int32_t *pairs,
+                     int unit) {
     const int64_t rows = g.nloc + g.nobj;
     const int npb = (LPG_DEFER_MAX * LPG_DEFER_MAX + 4 * kBlock - 1) / (4 * kBlock);   // one move per thread at the most
     hipLaunchKernelGGL(k_move_cols, dim3((unsigned)((rows + kBlock - 1) / kBlock + npb), 4), dim3(kBlock), 0,
-                       (hipStream_t)L.stream, g.T, g, st, D.Pbuf, pairs, npb);
+                       (hipStream_t)L.stream, g.T, g, st, D.Pbuf, pairs, npb, unit);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -176,6 +176,48 @@ def test_loaded_tableau_failing_the_unit_check_leaves_region_mode(lpg, monkeypat
     _assert_same(e, o, m)
 
 
+def test_loaded_tableau_with_negative_zero_in_a_basic_column_leaves_region_mode(lpg, monkeypatch):
+    """The unit check is bit for bit: a -0 in a basic column is not the +0 the
+    column trade writes for a leaving column's base data (k_move_cols writes
+    the unit vector without reading it), so such a tableau leaves region mode
+    and still solves bitwise the oracle."""
+    m, n = 300, 500
+    o0 = Oracle(m, n + m + 1)
+    o0.generate(n, 5, 0)
+    T = o0.get_rows().copy()
+    T[11, n + 1 + 3] = -0.0
+    basis = np.arange(n + 1, n + m + 1, dtype=np.int64)
+    o = Oracle(m, n + m + 1)
+    o.load_tableau(T, basis)
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=64)
+    e.load_tableau(T, basis)
+    res = e.solve(200_000, 0)
+    assert e.info.region == 0
+    ores = o.solve(200_000, 0)
+    assert res.status == ores.status and res.pivots == ores.pivots
+    _assert_same(e, o, m)
+
+
+@pytest.mark.parametrize("unit", ["0", "1"])
+@pytest.mark.parametrize("defer", [64, 96])
+def test_leaving_columns_written_as_unit_vectors(lpg, monkeypatch, unit, defer):
+    """The column trade's move of the leaving columns (k_move_cols) with their
+    base data read (LPG_MOVE_UNIT=0) or written as the unit vector of their
+    row (default in region blocks): bitwise the oracle either way, over whole
+    blocks with many trades."""
+    monkeypatch.setenv("LPG_MOVE_UNIT", unit)
+    m, n = 2048, 4096
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer)
+    o = Oracle(m, n + m + 1)
+    e.generate(n, 77, 0)
+    o.generate(n, 77, 0)
+    res = e.solve(5 * defer + 9, 0)
+    assert e.info.region == 1
+    ores = o.solve(5 * defer + 9, 0)
+    assert res.pivots == ores.pivots == 5 * defer + 9
+    _assert_same(e, o, m)
+
+
 @pytest.mark.parametrize("defer", [32, 96])
 @pytest.mark.parametrize("m,n,rule", [(120, 150, 0), (257, 300, 1)])
 def test_two_phase(lpg, monkeypatch, defer, m, n, rule):
