@@ -54,6 +54,12 @@ tools/probe/liblpg_phases.so: $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CS
 	@mkdir -p tools/probe
 	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip -ldl
 
+# publish / decision-seen stamps of every workgroup only (tools/block_probe.py PHASES_LIB=liblpg_pub.so)
+pub: tools/probe/liblpg_pub.so
+tools/probe/liblpg_pub.so: $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h
+	@mkdir -p tools/probe
+	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -DLPG_PHASES_PUBONLY -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip -ldl
+
 asm: $(CSRC)/lpg_kernels.hip
 	$(HIPCC) $(HIPFLAGS) -c --save-temps -o /tmp/lpg_kernels.o $(CSRC)/lpg_kernels.hip
 
@@ -62,4 +68,4 @@ clean:
 	rm -rf $(OBJDIR)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle ref asm clean phases
+.PHONY: all oracle ref asm clean phases pub

@@ -341,7 +341,8 @@ __device__ bool census(DevState *st, int nwg, uint32_t cl, const Xch &X, uint32_
 #ifdef LPG_PHASES
 // Phase probe (tools/block_probe.py; tools/liblpg_phases.so only): s_memrealtime
 // stamps of thread 0 of workgroups 0 and nwg / 2 at the phase boundaries of
-// every pivot of the launch.
+// every pivot of the launch (LPG_PHASES_PUBONLY: none of those, only every
+// workgroup's publish and decision-seen stamps, which cost each workgroup alike).
 __device__ unsigned long long g_bph[2][64][16];
 #ifdef LPG_PHASES_NOWAIT   // issue-time stamps: no wait for outstanding vector memory ops
 #define LPG_BPH_WAIT() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
@@ -349,6 +350,9 @@ __device__ unsigned long long g_bph[2][64][16];
 #define LPG_BPH_WAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
 #endif
 __device__ unsigned long long g_bclk[64];   // shader clock (clock64) beside workgroup 0's stamp 0
+#ifdef LPG_PHASES_PUBONLY
+#define LPG_BPH(t, k) do { } while (0)
+#else
 #define LPG_BPH(t, k)                                                                          \
     do {                                                                                       \
         LPG_BPH_WAIT();                                                                        \
@@ -357,21 +361,31 @@ __device__ unsigned long long g_bclk[64];   // shader clock (clock64) beside wor
             if ((k) == 0 && wg == 0) g_bclk[(t)] = clock64();                                  \
         }                                                                                      \
     } while (0)
+#endif
 __device__ unsigned long long g_bpub[2][64][256];   // every workgroup's publish stamp, phase P / S
+__device__ unsigned long long g_bseen[2][64][256];  // ... and when its wave 0 had swept the decision
 #define LPG_BPUB(ph, t)                                                                        \
     do {                                                                                       \
         if (tid == 0 && (t) < 64 && wg < 256) g_bpub[ph][(t)][wg] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+#define LPG_BSEEN(ph, t)                                                                       \
+    do {                                                                                       \
+        if (tid == 0 && (t) < 64 && wg < 256) g_bseen[ph][(t)][wg] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 int debug_block_phases(unsigned long long *out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bph), sizeof g_bph) != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out + sizeof g_bph / 8, HIP_SYMBOL(g_bpub), sizeof g_bpub) != hipSuccess) return -1;
-    return hipMemcpyFromSymbol(out + (sizeof g_bph + sizeof g_bpub) / 8, HIP_SYMBOL(g_bclk), sizeof g_bclk) == hipSuccess
+    if (hipMemcpyFromSymbol(out + (sizeof g_bph + sizeof g_bpub) / 8, HIP_SYMBOL(g_bclk), sizeof g_bclk) != hipSuccess)
+        return -1;
+    return hipMemcpyFromSymbol(out + (sizeof g_bph + sizeof g_bpub + sizeof g_bclk) / 8, HIP_SYMBOL(g_bseen),
+                               sizeof g_bseen) == hipSuccess
                ? 0
                : -1;
 }
 #else
 #define LPG_BPH(t, k) do { } while (0)
 #define LPG_BPUB(ph, t) do { } while (0)
+#define LPG_BSEEN(ph, t) do { } while (0)
 #endif
 
 // The pending chains of one thread over nb batches of 16 slots, software-
@@ -770,6 +784,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         }
         __syncthreads();
         LPG_BPH(t, 1);
+        LPG_BSEEN(1, t);                                // the ratio decision (records of phase S, t - 1)
         int okP = bc.ok;
         int64_t r = (int64_t)bc.p1;                     // leaving row (MR: this rank's candidate so far)
         const int64_t rs = r;                           // MR: the row computed ahead of the decision
@@ -1203,6 +1218,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         }
         __syncthreads();
         LPG_BPH(t, 4);
+        LPG_BSEEN(0, t);                                // the pricing decision (records of phase P, t)
         int okS = bc.ok;
         const int64_t kp = (int64_t)bc.p1;              // physical column of the entering column
         const double nR = __longlong_as_double((long long)bc.p0), nM = __longlong_as_double((long long)bc.p3);

@@ -17,9 +17,9 @@ import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
 
 from oracle.lpo import GEN_DEGENERATE, GEN_DENSE, RULE_BLAND, RULE_DANTZIG, Oracle
+from util import spawn_ranks
 
 
 def _protocol_worker(rank, world, port, m, n, seed, kind, rule, max_pivots, outdir):
@@ -62,15 +62,6 @@ def _protocol_worker(rank, world, port, m, n, seed, kind, rule, max_pivots, outd
         dist.destroy_process_group()
 
 
-def _free_port():
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 @pytest.mark.parametrize("world,m,n,kind,rule", [
     (2, 40, 64, GEN_DENSE, RULE_DANTZIG),
     (2, 33, 50, GEN_DEGENERATE, RULE_BLAND),
@@ -82,8 +73,7 @@ def _free_port():
 def test_gloo_row_partition_matches_single_process(world, m, n, kind, rule):
     seed, max_pivots = 12345, 4000
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_protocol_worker, args=(world, _free_port(), m, n, seed, kind, rule, max_pivots, d),
-                 nprocs=world, join=True)
+        spawn_ranks(_protocol_worker, lambda port: (world, port, m, n, seed, kind, rule, max_pivots, d), world)
         parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     ref = Oracle(m, n + m + 1)
     ref.generate(n, seed, kind)

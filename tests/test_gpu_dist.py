@@ -14,7 +14,6 @@ from __future__ import annotations
 
 import os
 import pickle
-import socket
 import tempfile
 import threading
 
@@ -22,7 +21,7 @@ import numpy as np
 import pytest
 
 from oracle.lpo import GEN_ARTIFICIAL, GEN_DUAL, Oracle
-from util import degenerate_two_phase_lp
+from util import degenerate_two_phase_lp, run_torchrun, spawn_ranks
 
 pytestmark = pytest.mark.gpu
 
@@ -206,15 +205,9 @@ def _gloo_worker(rank, world, port, m, n, seed, outdir, push=False, kind=0, rule
 
 def _processes(world, m, n, seed, push, kind=0, rule=0, defer=None, mr=None, big_m=False, two_phase=False, dual=False,
                region=None):
-    import torch.multiprocessing as mp
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_gloo_worker, args=(world, port, m, n, seed, d, push, kind, rule, defer, mr, big_m, two_phase, dual,
-                                     region),
-                 nprocs=world, join=True)
+        spawn_ranks(_gloo_worker, lambda port: (world, port, m, n, seed, d, push, kind, rule, defer, mr, big_m,
+                                                 two_phase, dual, region), world)
         parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     if big_m:
         o = Oracle(m, n + m + 1, nobj=2)
@@ -442,18 +435,14 @@ def test_bench_torchrun_4_ranks(world, exchange):
     (8 ranks passed on a fresh box, profiles/r03_pytest_gpu_4_8_ranks.log;
     see test_processes_4_ranks for why not in this suite)."""
     import json
-    import subprocess
     import sys
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(world),
-           "--config", "2", "--host-comm", "--exchange", exchange, "--steps", "4", "--warmup", "1", "--no-cpu"]
+    cmd = lambda port: [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(world),
+                        "--config", "2", "--host-comm", "--exchange", exchange, "--steps", "4", "--warmup", "1",
+                        "--no-cpu"]
     env = dict(os.environ, OMP_NUM_THREADS="1")
-    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    p = run_torchrun(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [x for x in p.stdout.splitlines() if x.strip()]
     assert len(lines) == 1, p.stdout[-2000:]
@@ -491,19 +480,15 @@ def test_push_on_one_gpu_refused_bench_falls_back(monkeypatch):
     falls back to the collectives before its first pivot -- the line reports
     the collectives and a normal run, not a mid-solve timeout."""
     import json
-    import subprocess
     import sys
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-           "--config", "2", "--host-comm", "--exchange", "push", "--steps", "2", "--warmup", "1", "--no-cpu"]
+    cmd = lambda port: [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--config", "2", "--host-comm", "--exchange", "push", "--steps", "2", "--warmup", "1",
+                        "--no-cpu"]
     env = {k: v for k, v in os.environ.items() if k not in ("LPG_PUSH_SHARED_DEVICE", "LPG_PUSH_SHARED_QUEUES")}
     env["OMP_NUM_THREADS"] = "1"
-    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    p = run_torchrun(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     assert "owner-push exchange refused: ranks" in p.stderr and "share GPU" in p.stderr, p.stderr[-3000:]
     lines = [x for x in p.stdout.splitlines() if x.strip()]

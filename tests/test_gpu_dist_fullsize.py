@@ -31,13 +31,13 @@ from __future__ import annotations
 
 import os
 import pickle
-import socket
 import tempfile
 
 import numpy as np
 import pytest
 
 from oracle.lpo import Oracle
+from util import spawn_ranks
 
 pytestmark = pytest.mark.gpu
 SEED = 20220518
@@ -127,14 +127,8 @@ def _worker(rank, world, port, m, n, seed, pivots, outdir, env, push, sample_row
 
 
 def _run(world, m, n, pivots, env, push=True, sample_rows=None, sweep=False):
-    import torch.multiprocessing as mp
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, port, m, n, SEED, pivots, d, env, push, sample_rows, sweep), nprocs=world,
-                 join=True)
+        spawn_ranks(_worker, lambda port: (world, port, m, n, SEED, pivots, d, env, push, sample_rows, sweep), world)
         return [pickle.load(open(os.path.join(d, f"r{q}.pkl"), "rb")) for q in range(world)]
 
 

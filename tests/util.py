@@ -74,3 +74,41 @@ def degenerate_two_phase_lp(m, n, seed):
     basis[m - 1] = art_first + 1
     T[m, 1:n + 1] = -(1 + rng.random(n))
     return T, basis, art_first
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _port_taken(text: str) -> bool:
+    return "EADDRINUSE" in text or "address already in use" in text
+
+
+def spawn_ranks(fn, make_args, nprocs, tries=3):
+    """torch.multiprocessing.spawn(fn, make_args(port), nprocs) on a fresh
+    127.0.0.1 port, again on another one if the rendezvous found the port
+    taken (a free port picked here can be taken before rank 0 listens on it)."""
+    import torch.multiprocessing as mp
+    for k in range(tries):
+        try:
+            mp.spawn(fn, args=make_args(free_port()), nprocs=nprocs, join=True)
+            return
+        except Exception as exc:   # ProcessRaisedException: the rank's traceback is in the text
+            if k + 1 == tries or not _port_taken(str(exc)):
+                raise
+
+
+def run_torchrun(make_cmd, tries=3, **kw):
+    """subprocess.run(make_cmd(port), ...) for a torch.distributed.run command,
+    again on another port if its rendezvous found the port taken."""
+    import subprocess
+    for k in range(tries):
+        r = subprocess.run(make_cmd(free_port()), **kw)
+        err = (r.stderr or "") if isinstance(r.stderr, str) else (r.stderr or b"").decode(errors="replace")
+        if r.returncode == 0 or k + 1 == tries or not _port_taken(err):
+            return r
