@@ -488,6 +488,7 @@ struct BlockArgs {
     uint32_t tag0;               // tag of pivot i of this launch = tag0 + 1 + i (never repeats per context)
     int nwg, cw, rw, ks;         // workgroups, columns / rows per slice, LDS slots
     uint32_t cl;                 // residency census: this launch's index since the DevState was reset (1-based)
+    int xcd1;                    // 1: a grid of 8 x nwg blocks of which blocks b % 8 == 0 work (one XCD, below)
     // REG (region mode): the slices hold the live columns only (below)
     const int32_t *live;         // nlive physical columns, nonbasic at the block start, column 0 excluded
     int64_t nlive;
@@ -568,7 +569,13 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     const Geo &g = a.g;
     const Defer &D = a.D;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wg = blockIdx.x, nwg = a.nwg, cw = a.cw, rw = a.rw, ks = a.ks;
+    // xcd1: blocks b and b + 8 share an XCD and its L2, so workgroup w runs as
+    // block 8 w and the other blocks leave at once: every record's store and
+    // load then stays on one XCD (0.98-1.21 us per sweep vs 1.33-1.50 over the
+    // chip at 16-32 workgroups, profiles/r05_sweep_lab_one_xcd.log). Speed only:
+    // the records keep their sc1 stores and loads, correct on any placement.
+    if (a.xcd1 && (blockIdx.x & 7)) return;
+    const int wg = a.xcd1 ? (int)(blockIdx.x >> 3) : (int)blockIdx.x, nwg = a.nwg, cw = a.cw, rw = a.rw, ks = a.ks;
     // thread-major slices: sP[col][slot], sC[row][slot], a row of S = slot_stride(ks)
     // doubles (>= ks + 8, = 2 mod 4: 16-byte reads of 16 consecutive lanes hit all
     // 64 banks once). Slots past the pending block stay +0, so the chains'
@@ -1538,11 +1545,25 @@ int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, in
     a.nsp = R ? R->nsp : 0;
     a.cwx = R ? R->cwx : cw;
     hipStream_t stream = (hipStream_t)L.stream;
+    // one XCD for grids that fit its CUs (one rank; LPG_PIVOT_XCD1=0 spreads them)
+    static const bool xcd1_on = [] {
+        const char *e = getenv("LPG_PIVOT_XCD1");
+        return !(e && e[0] == '0');
+    }();
+
     // the dynamic-LDS limit is a per-device attribute: set once per device
     // (bit `dev` of a per-kernel mask; ranks as threads may race to set it,
     // which is harmless)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+    static std::atomic<int> cus_of[64];   // CUs per device, read once (0: not yet)
+    int cus = cus_of[dev].load(std::memory_order_relaxed);
+    if (cus == 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = -1;
+        cus_of[dev].store(cus, std::memory_order_relaxed);
+    }
+    a.xcd1 = (xcd1_on && !X && cus >= 8 * 32 && nwg <= cus / 8) ? 1 : 0;
+    const unsigned grid = (unsigned)(a.xcd1 ? 8 * nwg : nwg);
 #define LPG_PB(RU, NO, M, KB, RG)                                                                       \
     do {                                                                                                \
         static std::atomic<unsigned long long> attr{0};                                                 \
@@ -1552,7 +1573,7 @@ int launch_pivot_block(const Launch &L, const Geo &g, int rule, DevState *st, in
                 return -1;                                                                              \
             attr.fetch_or(1ull << dev, std::memory_order_acq_rel);                                      \
         }                                                                                               \
-        hipLaunchKernelGGL((k_pivot_block<RU, NO, M, KB, RG>), dim3(nwg), dim3(kNT), lds, stream, a);  \
+        hipLaunchKernelGGL((k_pivot_block<RU, NO, M, KB, RG>), dim3(grid), dim3(kNT), lds, stream, a); \
     } while (0)
 #define LPG_PB_K(RU, NO, M, RG)                 \
     do {                                        \

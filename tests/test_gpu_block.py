@@ -112,8 +112,13 @@ def test_chain_batch_edges(lpg, monkeypatch, defer, m, n, seed, kind, rule):
     _assert_same(e, o, m)
 
 
+@pytest.mark.parametrize("xcd1", [None, "0"])
 @pytest.mark.parametrize("wg", [None, 17])
-def test_config2_to_optimality(lpg, monkeypatch, wg):
+def test_config2_to_optimality(lpg, monkeypatch, wg, xcd1):
+    """Config 2 to optimality, bitwise the oracle; its 13 (or 17) workgroups
+    run on one XCD (blocks 8 w of an 8 x nwg grid) or spread (LPG_PIVOT_XCD1=0)."""
+    if xcd1 is not None:
+        monkeypatch.setenv("LPG_PIVOT_XCD1", xcd1)
     m, n = 1024, 2048
     e = _engine(lpg, monkeypatch, m, n + m + 1, defer=32, wg=wg)
     assert e.info.pivot_wg > 0
