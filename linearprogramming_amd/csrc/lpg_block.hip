@@ -442,16 +442,18 @@ __device__ __forceinline__ double chain_n(const double *own, const double *uni, 
 template <bool ROW, bool SEL, bool B2>
 __device__ __forceinline__ double chain(const double *own, const double *uni, int nb, int lim, double x) {
 #ifndef LPG_CHAIN_UNROLL96
-#ifdef LPG_CHAIN_LOOP64
-    if (true) {
-#else
+#ifdef LPG_CHAIN_UNROLL64
     if (B2) {
+#else
+    if (true) {
 #endif
-        // 96-slot blocks: a loop over pairs of batches (then one), not a fully
-        // unrolled form per batch count -- those six bodies per chain kind made
-        // the launch's code (77 KB) larger than the instruction cache two CUs
-        // share (64 KB); each pair restarts the operand prefetch (one LDS round
-        // trip per 32 slots)
+        // a loop over pairs of batches (then one), not a fully unrolled form
+        // per batch count: at 96 slots those six bodies per chain kind made the
+        // launch's code (77 KB) larger than the instruction cache two CUs share
+        // (64 KB); at <= 64 slots the four bodies held 400-470 registers with
+        // spills, the loop 280-360 and none (config 5 68.7k -> 72.1k pivots/s,
+        // config 2 +0.9%, profiles/r05_ab_chain_loop64.log). Each pair restarts
+        // the operand prefetch (one LDS round trip per 32 slots)
         int b = 0;
 #pragma unroll 1
         for (; b + 2 <= nb; b += 2) x = chain_n<ROW, SEL, 2>(own + 16 * b, uni + 16 * b, lim - 16 * b, x);
