@@ -559,7 +559,13 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     // column}; the winner's {P_q[phys], j} granule (nwg + w) is fetched after
     // the sweep while the entering column's base entries load (j, the tie-break,
     // is read for every record that shares the least key -- rare)
-    constexpr bool PK1 = KDR;
+    // Bland on one objective row (round 5): the same one-granule sweep with the
+    // key = j (Bland's entering column is the least eligible j, and j is
+    // unique: no ties), and the winner's dR in a third granule (2 nwg + w),
+    // fetched after the sweep beside {P_q[k], j} -- the sweep read 3 granules
+    // per workgroup before
+    constexpr bool PK1 = NOBJ == 1;
+    constexpr bool PKD = PK1 && !KDR;                        // PK1 with the dR granule (Bland)
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ Bcast bc;
     __shared__ int xok;
@@ -618,7 +624,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
     const bool hr = tid < rw && i < g.nloc;
     const int64_t rM = g.nloc, rR = g.nloc + NOBJ - 1;
     const __amdgpu_buffer_rsrc_t recP = rsrc(a.rec, (nwg * NGP + 1) * 16);
-    const int xidx = PK1 ? 2 * nwg : nwg * NGP;                // workgroup 0's {P_q[0]} granule
+    const int xidx = PK1 ? (PKD ? 3 : 2) * nwg : nwg * NGP;     // workgroup 0's {P_q[0]} granule
     const __amdgpu_buffer_rsrc_t recR = rsrc(a.rec + nwg * kRecPMax, nwg * kRecR * 16);
     DevState *st = a.st;
 
@@ -1080,10 +1086,13 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         // and P_q[k] if it wins the grid); the thread of that column holds them
         if (PK1 && pb.j >= 0 && hc && (int64_t)lj == pb.j) {
             // the slice winner's thread: {key, physical column} and {P_q there, j}
-            const uint64_t h = ((uint64_t)(uint32_t)pb.cls << 63) |
-                               (~(uint64_t)__double_as_longlong(pb.v) & 0x7fffffffffffffffull);
+            // (PKD: key j, and {dR} in the third granule)
+            const uint64_t h = PKD ? (uint64_t)(uint32_t)pb.j
+                                   : (((uint64_t)(uint32_t)pb.cls << 63) |
+                                      (~(uint64_t)__double_as_longlong(pb.v) & 0x7fffffffffffffffull));
             rec_store(recP, wg * 16, pack(h, (uint32_t)c, tag));
             rec_store(recP, (nwg + wg) * 16, pack((uint64_t)__double_as_longlong(pq), (uint32_t)pb.j, tag));
+            if (PKD) rec_store(recP, (2 * nwg + wg) * 16, pack((uint64_t)__double_as_longlong(dR), 0u, tag));
         }
         if (!PK1 && pb.j >= 0 && hc && (int64_t)lj == pb.j) {
             rec_store(recP, (wg * NGP + 1) * 16, pack((uint64_t)__double_as_longlong(pq), (uint32_t)c, tag));
@@ -1120,6 +1129,7 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
 
         // ================= phase S: the entering column and the ratio test
         u4 g1{0u, 0u, 0u, 0u};                          // PK1, wave 0 lane 0: the winner's {P_q[k], j}
+        u4 g2{0u, 0u, 0u, 0u};                          // PKD, wave 0 lane 0: the winner's {dR}
         int g1src = -1;                                 // PK1, wave 0: its workgroup, -1 if fetched already / none
         if (wave == 0 && PK1) {
             u4 rec[kPer][1], xg{0u, 0u, 0u, 0u};
@@ -1152,8 +1162,13 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                     const int wl = __ffsll((long long)bal) - 1;
                     src = (int)rdl32((uint32_t)mw, wl);
                     p1 = rdl32(mphys, wl);
-                    if (lane == 0) g1 = rec_load(recP, (nwg + src) * 16);   // checked after the barrier
+                    if (lane == 0) {
+                        g1 = rec_load(recP, (nwg + src) * 16);   // checked after the barrier
+                        if (PKD) g2 = rec_load(recP, (2 * nwg + src) * 16);
+                    }
                     g1src = src;
+                } else if (PKD) {
+                    okd = -1;                           // Bland's keys are the columns' j: unique, never tied
                 } else {
                     // several records share the least key: j decides; fetch {P_q, j}
                     // of each (bounded polls), the least j wins
@@ -1230,7 +1245,8 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
         LPG_BSEEN(0, t);                                // the pricing decision (records of phase P, t)
         int okS = bc.ok;
         const int64_t kp = (int64_t)bc.p1;              // physical column of the entering column
-        const double nR = __longlong_as_double((long long)bc.p0), nM = __longlong_as_double((long long)bc.p3);
+        double nR = __longlong_as_double((long long)bc.p0);   // PKD: the fetched granule's, read below
+        const double nM = __longlong_as_double((long long)bc.p3);
         p0q = __longlong_as_double((long long)bc.z);
         // column k's base entries on this slice's rows (HBM) and P_u[k] for
         // u < q (Pbuf): in flight across the barrier below
@@ -1259,10 +1275,26 @@ __global__ __launch_bounds__(kNT, 1) void k_pivot_block(BlockArgs a) {
                     bc.l = g1.z;
                     bc.p2 = lo64(g1);
                 }
+                if (PKD) {                              // the winner's dR, stored with the other two
+                    while (g2.w != tag && (long long)wall_clock64() - t0 <= kSpinTicks) {
+                        __builtin_amdgcn_s_sleep(1);
+                        g2 = rec_load(recP, (2 * nwg + g1src) * 16);
+                    }
+                    if (g2.w != tag) {
+                        bc.ok = -1;
+                        st->stall_info[0] = 9;
+                        st->stall_info[1] = tag;
+                        st->stall_info[2] = 2 * nwg + g1src;
+                        st->stall_info[3] = g2.w;
+                    } else {
+                        bc.p0 = lo64(g2);
+                    }
+                }
             }
         }
         __syncthreads();
         okS = bc.ok;
+        if (PKD) nR = __longlong_as_double((long long)bc.p0);
         const int64_t kn = (int64_t)bc.l;               // logical entering column of pivot t + 1
         const double pkq = __longlong_as_double((long long)bc.p2);   // P_q at the entering column
         const int s1 = s ^ 1;
