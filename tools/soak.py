@@ -20,8 +20,11 @@ sys.path.insert(0, ROOT)
 import linearprogramming_amd as lpg  # noqa: E402
 from oracle.lpo import GEN_ARTIFICIAL, GEN_DEGENERATE, GEN_DENSE, GEN_DUAL, Oracle  # noqa: E402
 
+# per-context knobs (read at lpg_create); the process-wide ones (LPG_PIVOT_XCD1,
+# LPG_FLUSH_W96, LPG_FLUSH_ROWS, ...) are read once per process: set them for a
+# whole soak run instead
 KNOBS = ("LPG_DEFER", "LPG_PERSIST", "LPG_NO_REORDER", "LPG_FLUSH_KERNEL", "LPG_PERSIST_WG", "LPG_REGION",
-         "LPG_FLUSH_XCD", "LPG_FLUSH_TLIVE")
+         "LPG_FLUSH_XCD", "LPG_FLUSH_TLIVE", "LPG_MOVE_UNIT")
 
 
 def case(rng: random.Random, big: bool = False):
@@ -40,6 +43,7 @@ def case(rng: random.Random, big: bool = False):
         "LPG_REGION": rng.choice(["0", "1", "1"]),
         "LPG_FLUSH_XCD": rng.choice(["0", "1", "1", "h2", "h8"]),
         "LPG_FLUSH_TLIVE": rng.choice(["0", "1", "1"]),
+        "LPG_MOVE_UNIT": rng.choice(["0", "1", "1"]),
     }
     if rng.random() < 0.3:
         env["LPG_PERSIST_WG"] = str(rng.choice([8, 16, 32, 64, 128]))
