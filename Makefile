@@ -11,11 +11,19 @@ LIB       = linearprogramming_amd/liblpg.so
 
 
 OBJDIR    = build/obj
-KOBJS     = $(OBJDIR)/lpg_kernels.o $(OBJDIR)/lpg_block.o $(OBJDIR)/lpg_dual.o
+KOBJS     = $(OBJDIR)/lpg_kernels.o $(OBJDIR)/lpg_block.o $(OBJDIR)/lpg_dual.o $(OBJDIR)/lpg_stamp.o
 HDRS      = $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h include/lpg.h
 HOOKLIB   = linearprogramming_amd/liblpg_testhooks.so
+# the source stamp compiled into the library (lpg_build_stamp; _lib.load()
+# refuses a library whose stamp is not the sources')
+STAMP    := $(shell python3 linearprogramming_amd/_stamp.py)
 
 all: $(LIB) $(HOOKLIB) host/lpgcli oracle
+
+$(OBJDIR)/lpg_stamp.o: $(wildcard $(CSRC)/*.hip) $(HDRS) linearprogramming_amd/_stamp.py
+	@mkdir -p $(OBJDIR)
+	printf '#include "lpg.h"\nconst char *lpg_build_stamp(void) { return "%s"; }\n' '$(STAMP)' > $(OBJDIR)/lpg_stamp.c
+	$(CC) -O2 -fPIC -Iinclude -c -o $@ $(OBJDIR)/lpg_stamp.c
 
 # one object per translation unit (no cross-TU device code: every kernel is
 # launched from the file that defines it), so the product library and the
@@ -50,15 +58,15 @@ ref:
 # phase-stamped build for tools/phase_probe.py and tools/block_probe.py
 # (diagnostics only; tools/probe/ travels to the GPU box, delete it when done)
 phases: tools/probe/liblpg_phases.so
-tools/probe/liblpg_phases.so: $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h
+tools/probe/liblpg_phases.so: $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h $(OBJDIR)/lpg_stamp.o
 	@mkdir -p tools/probe
-	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip -ldl
+	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(OBJDIR)/lpg_stamp.o -ldl
 
 # publish / decision-seen stamps of every workgroup only (tools/block_probe.py PHASES_LIB=liblpg_pub.so)
 pub: tools/probe/liblpg_pub.so
-tools/probe/liblpg_pub.so: $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h
+tools/probe/liblpg_pub.so: $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h $(OBJDIR)/lpg_stamp.o
 	@mkdir -p tools/probe
-	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -DLPG_PHASES_PUBONLY -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip -ldl
+	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -DLPG_PHASES_PUBONLY -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(OBJDIR)/lpg_stamp.o -ldl
 
 asm: $(CSRC)/lpg_kernels.hip
 	$(HIPCC) $(HIPFLAGS) -c --save-temps -o /tmp/lpg_kernels.o $(CSRC)/lpg_kernels.hip

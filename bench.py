@@ -6,9 +6,11 @@ the device (splitmix64, seed 20220518). Each simplex pivot is price (argmin
 over the reduced-cost row) -> ratio test (min over the entering column) ->
 Gauss-Jordan rank-1 update of the whole tableau. The update is deferred:
 prep / select evaluate the pending chain for the entries they need and
-k_flushw applies each block of K pivots (LPG_DEFER; 96 for tableaus >= 16 GB
-per rank, 64 from 200 MB, else 32) to the constraint rows in one HBM pass,
-bitwise identical to K eager updates.
+k_flushw applies each block of K pivots to the constraint rows in one pass,
+bitwise identical to K eager updates (LPG_DEFER; default K = 96 in region
+mode from 2 GB on one rank / 1 GB per rank of a partition -- config 3 --, 96
+from 16 GB with the two-kernel pair -- config 4 --, 64 from 200 MB, else 32;
+include/lpg.h).
 
 A "step" is one such block: K pivots and the one pass over the tableau that
 applies them (with --defer 0, eager updates, a step is one pivot). `value` is
@@ -42,11 +44,65 @@ import os
 import sys
 import time
 
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def spawn_ranks_if_needed() -> None:
+    """`python3 bench.py --gpus N` with N > 1 and no WORLD_SIZE in the
+    environment: start N rank processes of this same command (RANK /
+    LOCAL_RANK / WORLD_SIZE set, rendezvous through a file in a fresh
+    temporary directory, so no port can collide), relay rank 0's one JSON line
+    on stdout and exit with the first failing rank's code. Runs before this
+    process imports the engine, torch or anything that could touch the GPU
+    (VERDICT r5 missing #3); the torch.distributed.run launch is unchanged."""
+    if "WORLD_SIZE" in os.environ:
+        return
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    n = ap.parse_known_args()[0].gpus
+    if n <= 1:
+        return
+    import subprocess
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="lpg_bench_")
+    out_path = os.path.join(tmp, "rank0.out")
+    procs = []
+    with open(out_path, "wb") as out0:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       MASTER_ADDR="127.0.0.1", LPG_BENCH_INIT_FILE=os.path.join(tmp, "rendezvous"))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                          stdout=out0 if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:                      # one rank failed: the others would wait on it in a collective
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+        rc = rc or p.returncode
+    with open(out_path, "rb") as f:
+        sys.stdout.buffer.write(f.read())
+    sys.stdout.flush()
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
+    raise SystemExit(rc)
+
+
+if __name__ == "__main__":
+    spawn_ranks_if_needed()
+
 import linearprogramming_amd as lpg   # first: binds the process to the system ROCm runtime (_lib.bind_runtime)
 import torch  # noqa: E402  (torch.distributed gloo plumbing only; reuses that runtime)
 import torch.distributed as dist  # noqa: E402
+from linearprogramming_amd import _lib as lpg_lib  # noqa: E402
+from linearprogramming_amd._stamp import source_stamp  # noqa: E402
 
-ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "Simplex pivots/sec + HBM GB/s fraction, dense m=16384×n=32768 fp64, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 # dense f64 matrix-core peak of MI355X (AMD's published FP64 matrix figure, no
@@ -80,22 +136,6 @@ CONFIGS = {
     5: dict(m=8192, n=8192, name="BASELINE config 5: two-phase (artificials) on a KM-style degenerate LP m=8192 n=8192, "
                                  "Bland rule, pivot cap 20000"),
 }
-
-
-def source_stamp() -> str:
-    """Hash of the engine's sources (csrc/*.hip, csrc/*.h, include/lpg.h): a PMC
-    traffic file is attached only to a bench line of the build it measured."""
-    import glob
-    import hashlib
-    h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(ROOT, "linearprogramming_amd", "csrc", "*.hip")) +
-                   glob.glob(os.path.join(ROOT, "linearprogramming_amd", "csrc", "*.h")) +
-                   [os.path.join(ROOT, "include", "lpg.h")])
-    for f in files:
-        h.update(os.path.basename(f).encode())
-        with open(f, "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
 
 
 def pmc_traffic(a, kname, defer, m, n, world, stamp):
@@ -182,6 +222,46 @@ def cpu_baseline(m, n, gpu_log, budget_s, budget_1core_s):
             "sample": f"{done} timed pivots (after 1 untimed) of the same {m}x{n} LP, oracle/liblpo.so "
                       f"(C fp64, OpenMP {threads} threads)",
             "seconds": dt, "single_core": one}, {"pivots_compared": int(n_cmp), "identical_pivot_sequence": same}
+
+
+def trajectory_parity(a, eng, world, rank):
+    """The whole run -- warm-up and timed pivots -- against the oracle's pinned
+    trajectory of config 3 (tests/golden/config3_2400.json, VERDICT r5 missing
+    #2): the (entering, leaving) log pivot by pivot, and at the run's last
+    pivot (a multiple of 96 up to 2,400: the default and the driver's forms
+    both end on one) the objective's bits, the basis and the digests of column
+    0, the objective row and 16 fixed rows (rows at N = 1 only). Read after
+    the timed region. None for other configs / shapes."""
+    if a.config != 3 or a.shape:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    try:
+        import trajectory as T
+    finally:
+        sys.path.pop(0)
+    if not os.path.exists(T.FIXTURE):
+        return {"error": "tests/golden/config3_2400.json missing"}
+    import numpy as np
+    fix = T.load()
+    k, r = eng.get_log()
+    res = eng.sync()
+    snaps = {}
+    key = str(res.pivots)
+    if key in fix["checkpoints"]:
+        if world == 1:
+            rows = np.concatenate([eng.get_rows(i, 1) for i in T.ROWS])
+            snaps[res.pivots] = T.snapshot(res.objective, eng.get_basis(), eng.get_column0(),
+                                           eng.get_rows(T.M, 1)[0], rows)
+        else:                                        # the replicated parts only; rows live on their owners
+            snaps[res.pivots] = {"objective_hex": float(res.objective).hex(), "basis": T.digest(eng.get_basis())}
+    cmp = T.compare(fix, k, r, snaps)
+    cmp.update({"fixture": "tests/golden/config3_2400.json (oracle/liblpo.so, tests/golden/make_config3_golden.py)",
+                "pivots_run": int(res.pivots),
+                "covers_timed_region": bool(cmp["pivots_compared"] >= res.pivots and cmp["pivots_compared"] > 0),
+                "rows_checked": world == 1 and bool(snaps)})
+    if world > 1:
+        cmp["note"] = "N > 1: log, objective and basis (replicated) checked; row digests at N = 1"
+    return cmp if rank == 0 else None
 
 
 def host_ops(world):
@@ -289,7 +369,9 @@ def main():
         result_fd = os.dup(1)
         os.dup2(2, 1)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init = os.environ.get("LPG_BENCH_INIT_FILE")      # the self-spawned ranks (spawn_ranks_if_needed)
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                init_method=f"file://{init}" if init else None)
     cfg = CONFIGS[a.config]
     m, n = cfg["m"], cfg["n"]
     if a.shape:                                        # a stand-in shape, labelled as such in the line
@@ -492,6 +574,10 @@ def main():
         "pivots_total": res.pivots,
         "objective": res.objective,
     }
+    line["build_stamp"] = lpg_lib.build_stamp
+    traj = trajectory_parity(a, eng, world, rank)
+    if traj is not None:
+        line["parity_trajectory"] = traj
     if world == 1 and rank == 0 and not a.no_cpu:
         log = eng.get_log()
         eng.close()

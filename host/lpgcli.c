@@ -230,13 +230,34 @@ static int run_rank(const dist_args *a, int rank, int fd) {
         (rc = lpg_comm_init_host(ctx, &ops)) != 0)
         goto fail;
     if (a->push) {
-        char mine[LPG_PUSH_HANDLE_BYTES];
+        /* every rank attaches the owner push, or none does: the attach is
+         * refused where ranks share a GPU (lpg.h), possibly on some ranks only
+         * (3 ranks on 2 GPUs), so the ranks agree on an ok flag and, if any was
+         * refused, all of them rebuild their context on the host collectives
+         * (the caller keeps the collectives, lpg.h) -- exchange 0 in the line */
+        char mine[LPG_PUSH_HANDLE_BYTES], ok, oks[256];
         char *all = (char *)malloc((size_t)a->world * LPG_PUSH_HANDLE_BYTES);
-        rc = all ? lpg_comm_push_handle(ctx, mine, sizeof mine) : LPG_ERR_OOM;
-        if (!rc) rc = cb_allgather(&h, mine, all, sizeof mine) ? LPG_ERR_COMM : 0;
-        if (!rc) rc = lpg_comm_init_push(ctx, all, (size_t)a->world * LPG_PUSH_HANDLE_BYTES);
+        if (!all || a->world > 256) { free(all); rc = LPG_ERR_OOM; goto fail; }
+        rc = lpg_comm_push_handle(ctx, mine, sizeof mine);
+        ok = rc == 0;
+        if (cb_allgather(&h, &ok, oks, 1)) { free(all); rc = LPG_ERR_COMM; goto fail; }
+        for (int q = 0; q < a->world; q++) ok = ok && oks[q];
+        if (ok && cb_allgather(&h, mine, all, sizeof mine)) { free(all); rc = LPG_ERR_COMM; goto fail; }
+        if (ok) {
+            rc = lpg_comm_init_push(ctx, all, (size_t)a->world * LPG_PUSH_HANDLE_BYTES);
+            if (rc) fprintf(stderr, "lpgcli: rank %d: %s; using the host collectives\n", rank, lpg_last_error(ctx));
+            ok = rc == 0;
+            if (cb_allgather(&h, &ok, oks, 1)) { free(all); rc = LPG_ERR_COMM; goto fail; }
+            for (int q = 0; q < a->world; q++) ok = ok && oks[q];
+        }
         free(all);
-        if (rc) goto fail;
+        if (!ok) {
+            lpg_destroy(ctx);
+            ctx = NULL;
+            if ((rc = lpg_create_dist(&ctx, dev, a->world, rank, a->m, a->n + a->m + 1, 0)) != 0 ||
+                (rc = lpg_comm_init_host(ctx, &ops)) != 0)
+                goto fail;
+        }
     }
     if ((rc = lpg_generate(ctx, a->n, a->seed, a->dual ? LPG_GEN_DUAL : a->kind)) != 0) goto fail;
     char one = 1, got[256];

@@ -83,10 +83,14 @@ extern "C" {
 #define LPG_FLAG_EAGER   0x8u  /* one rank-1 update pass per pivot instead of deferred (blocked) updates */
 
 /* Deferred updates (default): the constraint rows are brought up to date in
- * one HBM pass per block of up to LPG_DEFER_MAX pivots (96 when a rank's
- * tableau is >= 16 GB, 64 when >= 200 MB, else 32; env LPG_DEFER=K picks K,
- * K in 1 .. 128; 0 = eager; the persistent pivot kernel takes blocks of at
- * most 64). Values,
+ * one HBM pass per block of up to LPG_DEFER_MAX pivots. Default K (decided
+ * from the largest rank's tableau bytes): 96 in region mode (lpg_info.region)
+ * from 2 GB on one rank and from 1 GB on the ranks of a row partition, where
+ * the region-mode slices hold 96 slots (config 3); 96 from 16 GB (the
+ * two-kernel pair, config 4); 64 from 200 MB; 32 below. Env LPG_DEFER=K picks
+ * K, K in 1 .. 128; 0 = eager. The persistent pivot kernel takes blocks of up
+ * to 96 slots where its slices fit (lpg_info.pivot_wg > 0), else the pair
+ * runs the pivots. Values,
  * pivot sequence and log are bitwise those of eager updates; every call that
  * reads or replaces the tableau (lpg_get_rows, lpg_get_column0, lpg_load_rows,
  * lpg_set_basis, lpg_set_objective*, lpg_sync, lpg_device_sync, the end of
@@ -129,6 +133,8 @@ typedef struct {
                                    block start's nonbasic columns plus a spare slot per pending pivot for the
                                    column leaving the basis then (one rank, one objective row, column trade on;
                                    the default where it fits, env LPG_REGION=0 turns it off) */
+    int32_t region_recoveries;  /* region-mode launches that found a block's column trade incomplete
+                                   (DevState::rbad), ran no pivot and were re-run after a region rebuild */
 } lpg_info_t;
 
 typedef struct {
@@ -176,7 +182,8 @@ int  lpg_comm_init_host(lpg_ctx *ctx, const lpg_host_comm_ops *ops);
  * between ranks of one process (lpg_comm_push_base -> lpg_comm_init_push_local).
  * Waits are bounded (2 s): a rank that waits longer ends the solve with
  * LPG_NUMERIC and lpg_last_error names the exchange. With the push attached,
- * blocks of <= 64 pivots run as one persistent launch per block on every
+ * each block (<= 96 pivots; region mode with K = 96 from 1 GB per rank, see
+ * above) runs as one persistent launch per block on every
  * rank (lpg_info.pivot_wg > 0; each rank needs its own GPU, or launches
  * small enough to be resident together; env LPG_PERSIST_MR=0: two kernels
  * per pivot). The exchange's kernels spin-wait on their peers, so attaching
@@ -195,6 +202,11 @@ int  lpg_comm_init_push_local(lpg_ctx *ctx, void *const *bases, int world);
 void lpg_destroy(lpg_ctx *ctx);
 int  lpg_info(const lpg_ctx *ctx, lpg_info_t *out);
 const char *lpg_last_error(const lpg_ctx *ctx);
+/* The source stamp this library was built from (16 hex digits: sha256 over
+ * the engine's csrc/ files and this header, linearprogramming_amd/_stamp.py).
+ * No reference counterpart: a loader compares it with the sources beside the
+ * library and refuses a stale binary. */
+const char *lpg_build_stamp(void);
 
 /* ---- loading (host buffers are copied) ---- */
 /* Rows [row0, row0+nrows) in GLOBAL numbering, each [b | a_1..a_N] with pitch

@@ -93,6 +93,7 @@ struct lpg_ctx {
     uint32_t pb_launch = 0;       // persistent launches since the DevState was reset (the census index)
     int64_t lost = 0;             // pivots enqueued on launches a residency census stopped (lpg_sync re-runs them)
     int res_fallbacks = 0;        // residency censuses that failed (lpg_info: the pair took over)
+    int reg_recoveries = 0;       // region-mode launches stopped by rbad and re-run (recover_region)
     // owner-push exchange of the multi-rank deferred path (Xch, lpg_internal.h)
     char *xbuf = nullptr;         // this rank's exchange buffer
     int64_t xbytes = 0, xoffF = 0, xoffC = 0, xoffG = 0;
@@ -136,6 +137,11 @@ struct lpg_ctx {
     // before flush F, make the pending block inconsistent (W = npend | kq | lv |
     // rq | ahead) to exercise k_swap_plan's guard
     int inject_flush = -1, inject_what = 0;
+    // (test hooks) env LPG_TEST_REGION_BAD=F: after flush F's swap plan, set
+    // DevState::rbad as an incomplete column trade would, so that the next
+    // region-mode launch -- inside the same lpg_enqueue -- stops with
+    // kStallRegion and recover_region / lpg_sync re-run its pivots
+    int inject_rbad = -1;
     // k_swap_plan refused a pending block (pending_fault): the basis already
     // holds the block's pivots while the constraint rows do not, so every
     // pivoting entry point refuses until the LP is reloaded or regenerated
@@ -396,6 +402,10 @@ static int flush_launch(lpg_ctx *c) {
     if (launch_swap_plan(lau(c), geo(c), c->st, defer_of(c, 0), c->colmap, c->inv, c->pairs, re ? 1 : 0, c->defer_k) ||
         (re && launch_move_cols(lau(c), geo(c), c->st, defer_of(c, 0), c->pairs, unit)))
         return fail(c, LPG_ERR_DEVICE, "swap plan launch failed");
+#ifdef LPG_TEST_HOOKS
+    if (c->inject_rbad >= 0 && c->nflush == c->inject_rbad + 1)
+        HIPCHK(c, hipMemsetAsync(&c->st->rbad, 0x01, sizeof(uint32_t), c->stream));
+#endif
     if (c->timing && ((rc = timing_mark(c, 0)) || (rc = timing_mark(c, 1)))) return rc;
     // tlive: region blocks only (every pivot recorded its leaving column, the
     // basic columns were exact unit vectors at the block start); LPG_FLUSH_TLIVE=0 off (A/B)
@@ -864,6 +874,7 @@ static int recover_residency(lpg_ctx *c, const DevState &h) {
 // caller's column order, then rebuilding the region, which clears rbad) and
 // lpg_sync re-runs the lost pivots, as after a residency abort.
 static int recover_region(lpg_ctx *c, const DevState &h) {
+    c->reg_recoveries++;
     c->lost += std::max<int64_t>(c->enq - h.pivots, 0);
     c->enq = h.pivots;
     c->pend = (int)h.npend;
@@ -886,13 +897,15 @@ static int pending_fault(lpg_ctx *c, const DevState &h) {
 }
 
 // Every pivoting entry point: a context whose pending block was refused
-// (pending_fault) stays refused until lpg_load_rows / lpg_generate rewrite
-// the tableau (continuing would pivot on a basis and constraint
-// rows that disagree).
+// (pending_fault) stays refused until the basis is replaced (lpg_set_basis,
+// normally after lpg_load_rows) or the LP regenerated (lpg_generate)
+// (continuing would pivot on a basis and constraint rows that
+// disagree; ADVICE r5: a row reload alone no longer clears it).
 static int usable(lpg_ctx *c) {
     if (!c->poisoned) return 0;
     return fail(c, LPG_ERR_STATE, "context unusable: an earlier flush refused an inconsistent pending block, so the "
-                "basis and the constraint rows disagree; reload (lpg_load_rows) or regenerate (lpg_generate) the LP");
+                "basis and the constraint rows disagree; reload the rows and the basis (lpg_load_rows, lpg_set_basis) or "
+                "regenerate (lpg_generate) the LP");
 }
 
 static int read_result(lpg_ctx *c, lpg_result *out, int rule) {
@@ -1094,6 +1107,7 @@ int lpg_create_dist(lpg_ctx **out, int device, int world, int rank, int64_t m, i
             c->inject_flush = c->inject_what ? f : -1;
         }
     }
+    if (const char *rb = getenv("LPG_TEST_REGION_BAD")) c->inject_rbad = atoi(rb);
 #endif
     const char *fv = getenv("LPG_FLUSH_KERNEL");   // m | w: force k_flushm / k_flushw (tests); default by block size
     c->flush_variant = fv ? (fv[0] == 'w' ? 1 : fv[0] == 'm' ? 0 : -1) : -1;
@@ -1348,12 +1362,16 @@ static int push_shares_device(lpg_ctx *c, const std::vector<char *> &bases) {
     for (int r = 0; r < c->world; r++) {
         if (r == c->rank) continue;
         HIPCHK(c, hipMemcpy(peer, bases[r] + c->xoffG + kXchIdOff, sizeof peer, hipMemcpyDeviceToHost));
-        if (peer[0] && !strncmp(mine, peer, 48))
+        if (peer[0] && !strncmp(mine, peer, 48)) {
+            int32_t pid_mine, pid_peer;      // the owning processes, named in the message
+            memcpy(&pid_mine, mine + 48, sizeof pid_mine);
+            memcpy(&pid_peer, peer + 48, sizeof pid_peer);
             return fail(c, LPG_ERR_STATE,
-                        "owner-push exchange refused: ranks %d and %d share GPU %.48s, so a rank's spin-waiting "
-                        "exchange kernel can hold the CUs its peer needs; use one GPU per rank, or the collectives "
-                        "(LPG_PUSH_SHARED_DEVICE=1 acknowledges the sharing for small co-resident tests)",
-                        c->rank, r, mine);
+                        "owner-push exchange refused: ranks %d (pid %d) and %d (pid %d) share GPU %.48s, so a rank's "
+                        "spin-waiting exchange kernel can hold the CUs its peer needs; use one GPU per rank, or the "
+                        "collectives (LPG_PUSH_SHARED_DEVICE=1 acknowledges the sharing for small co-resident tests)",
+                        c->rank, (int)pid_mine, r, (int)pid_peer, mine);
+        }
     }
     return 0;
 }
@@ -1473,6 +1491,7 @@ int lpg_info(const lpg_ctx *c, lpg_info_t *o) {
     o->exchange = c->xmode ? (c->xuncached ? 2 : 1) : 0;
     o->column_trade = reorders(c) ? 1 : 0;
     o->residency_fallbacks = c->res_fallbacks;
+    o->region_recoveries = c->reg_recoveries;
     o->region = (o->pivot_wg > 0 && c->reg) ? 1 : 0;
     return 0;
 }
@@ -1497,7 +1516,9 @@ int lpg_load_rows(lpg_ctx *c, int64_t row0, int64_t nrows, const double *rows, i
             HIPCHK(c, hipMemcpy(c->T + (c->nloc + q) * c->ld, rows + (gi - row0) * ld, c->ncols * sizeof(double),
                                 hipMemcpyHostToDevice));
     }
-    c->poisoned = false;   // the caller rewrites the tableau (its pending block was cleared at the refusal)
+    // (a refused context stays refused: rows alone, even all of them, do not
+    // replace the basis that holds the refused block's pivots -- lpg_set_basis
+    // or lpg_generate clears it)
     c->units_known = false;   // region mode checks the basic columns first (region_setup)
     return reset_state(c);
 }
@@ -1511,6 +1532,7 @@ int lpg_set_basis(lpg_ctx *c, const int64_t *basis) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(c->basis, basis, c->m * sizeof(int64_t), hipMemcpyHostToDevice));
     c->units_known = false;
+    c->poisoned = false;   // the caller's basis replaces the one holding a refused block's pivots
     return reset_state(c);
 }
 

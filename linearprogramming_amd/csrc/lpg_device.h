@@ -150,7 +150,13 @@ __device__ __forceinline__ uint64_t dpp64(uint64_t v) {
 __device__ __forceinline__ uint64_t min64(uint64_t a, uint64_t b) { return b < a ? b : a; }
 
 // the same move where every lane of every row takes a source lane (quad_perm,
-// mirrors): no old value to keep, so no copy in front of the DPP move
+// mirrors): no old value to keep, so no copy in front of the DPP move.
+// PRECONDITION (every wave_min_* / wave_min_key below): the whole wave is
+// active (EXEC = all 64 lanes). With bound_ctrl and no old value, a lane
+// reading a disabled source lane gets 0, and 0 would become the "minimum";
+// call these only from wave-uniform control flow (every caller in
+// lpg_block.hip / lpg_kernels.hip / lpg_dual.hip does: out-of-range lanes
+// take the neutral key ~0 instead of leaving the branch). ADVICE r5.
 template <int CTRL>
 __device__ __forceinline__ uint64_t dpp64f(uint64_t v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, true);

@@ -22,10 +22,8 @@ from oracle.lpo import GEN_DEGENERATE, GEN_DENSE, RULE_BLAND, RULE_DANTZIG, Orac
 from util import spawn_ranks
 
 
-def _protocol_worker(rank, world, port, m, n, seed, kind, rule, max_pivots, outdir):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _protocol_worker(rank, world, init, m, n, seed, kind, rule, max_pivots, outdir):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         full = Oracle(m, n + m + 1)
         full.generate(n, seed, kind)
@@ -73,7 +71,7 @@ def _protocol_worker(rank, world, port, m, n, seed, kind, rule, max_pivots, outd
 def test_gloo_row_partition_matches_single_process(world, m, n, kind, rule):
     seed, max_pivots = 12345, 4000
     with tempfile.TemporaryDirectory() as d:
-        spawn_ranks(_protocol_worker, lambda port: (world, port, m, n, seed, kind, rule, max_pivots, d), world)
+        spawn_ranks(_protocol_worker, lambda init: (world, init, m, n, seed, kind, rule, max_pivots, d), world)
         parts = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
     ref = Oracle(m, n + m + 1)
     ref.generate(n, seed, kind)

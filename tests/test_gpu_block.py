@@ -321,6 +321,12 @@ def test_inconsistent_pending_block_stops_numeric(lpg, monkeypatch, what, persis
         e.solve(40 if what == "ahead" else 100_000, 0)
     with pytest.raises(lpg.LPGError, match=r"context unusable"):
         e.solve(100_000, 0)
+    if what == "npend" and persist is None:
+        # a partial (here one-row) reload keeps it refused; only a
+        # replaced basis or a regenerated LP clears it
+        e.load_rows(0, e.get_rows(0, 1))
+        with pytest.raises(lpg.LPGError, match=r"context unusable"):
+            e.solve(100_000, 0)
     e.generate(n, 5, 0)                                # a rewritten tableau: usable again
     res = e.solve(100_000, 0)
     o = Oracle(m, n + m + 1)

@@ -32,11 +32,13 @@ def _fnv(k, r):
     return f"{h:016x}"
 
 
-def _cli(args, env=None, timeout=120):
+def _cli(args, env=None, timeout=120, ack_shared=True):
     # `--gpus P` forks P ranks onto the test box's ONE GPU: acknowledge that for
     # the owner push (refused at attach otherwise, lpg_ctx.hip push_shares_device)
-    p = subprocess.run([CLI] + args, capture_output=True, text=True, timeout=timeout,
-                       env={**os.environ, "LPG_PUSH_SHARED_DEVICE": "1", **(env or {})})
+    base = {k: v for k, v in os.environ.items() if k not in ("LPG_PUSH_SHARED_DEVICE", "LPG_PUSH_SHARED_QUEUES")}
+    if ack_shared:
+        base["LPG_PUSH_SHARED_DEVICE"] = "1"
+    p = subprocess.run([CLI] + args, capture_output=True, text=True, timeout=timeout, env={**base, **(env or {})})
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     return p, lines
 
@@ -80,6 +82,29 @@ def test_gpus_equals_one_rank_and_the_oracle(m, n, gpus, extra, env):
     res = o.solve(int(extra[extra.index("--pivots") + 1]) if "--pivots" in extra else 1 << 40, 1 if "bland" in extra else 0)
     assert res.pivots == one["pivots"] and res.objective == one["objective"]
     assert _fnv(*o.get_log()) == one["log_fnv"]
+
+
+@needs_cli
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpus", [2, 3])
+def test_gpus_refused_push_falls_back_to_host_collectives(gpus):
+    """the README's `lpgcli --synthetic 1024 2048 --gpus 2`
+    on a node with fewer GPUs than ranks, without the test override. The
+    owner push is refused at attach (ranks share a GPU); every rank must then
+    continue on the host collectives (exchange 0), not exit -- also when the
+    refusal would be asymmetric (3 ranks)."""
+    m, n = 1024, 2048
+    p1, l1 = _cli(["--synthetic", str(m), str(n)])
+    assert p1.returncode == 0, p1.stderr
+    one = json.loads(l1[-1])
+    pp, lp = _cli(["--synthetic", str(m), str(n), "--gpus", str(gpus)], ack_shared=False)
+    assert pp.returncode == 0, pp.stderr
+    assert "using the host collectives" in pp.stderr and "share GPU" in pp.stderr, pp.stderr
+    assert len(lp) == 1, lp
+    dist = json.loads(lp[0])
+    assert dist["exchange"] == 0 and dist["gpus"] == gpus
+    assert dist["pivots"] == one["pivots"] and dist["objective"] == one["objective"]
+    assert dist["log_fnv"] == one["log_fnv"]
 
 
 @needs_cli

@@ -68,13 +68,11 @@ def _sample(m, world, rank, k, seed):
     return sorted(set(rng.choice(np.arange(r0, r1), k, replace=False).tolist()) | {r0, r1 - 1})
 
 
-def _worker(rank, world, port, m, n, seed, pivots, outdir, env, push, sample_rows=None, sweep=False):
+def _worker(rank, world, init, m, n, seed, pivots, outdir, env, push, sample_rows=None, sweep=False):
     os.environ.update(env)
     import torch
     import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     import linearprogramming_amd as lpg
 
     def allgather(b: bytes) -> bytes:
@@ -128,7 +126,7 @@ def _worker(rank, world, port, m, n, seed, pivots, outdir, env, push, sample_row
 
 def _run(world, m, n, pivots, env, push=True, sample_rows=None, sweep=False):
     with tempfile.TemporaryDirectory() as d:
-        spawn_ranks(_worker, lambda port: (world, port, m, n, SEED, pivots, d, env, push, sample_rows, sweep), world)
+        spawn_ranks(_worker, lambda init: (world, init, m, n, SEED, pivots, d, env, push, sample_rows, sweep), world)
         return [pickle.load(open(os.path.join(d, f"r{q}.pkl"), "rb")) for q in range(world)]
 
 

@@ -253,6 +253,36 @@ def test_two_phase_forced_drive_out(lpg, monkeypatch, defer):
     _assert_same(e, o, m)
 
 
+@pytest.mark.parametrize("flush", [0, 2])
+def test_region_stall_mid_enqueue_recovers_bitwise(lpg, monkeypatch, flush):
+    """the kStallRegion path itself. A forced pivot is always
+    followed by a bootstrap that rebuilds the region before any launch reads
+    rbad, so the drive-out test above never stalls. The test-hook build
+    (liblpg_testhooks.so) sets rbad after block `flush`'s swap plan, as an
+    incomplete column trade would, in the middle of ONE lpg_enqueue: the next
+    region launch runs no pivot (neither does any launch after it),
+    recover_region counts it, and lpg_sync re-runs the lost pivots after a
+    region rebuild -- pivot count, log, basis and whole tableau the oracle's."""
+    from linearprogramming_amd import _lib as L
+    m, n, K = 700, 1300, 32
+    hooks = L.load_testhooks()
+    monkeypatch.setenv("LPG_TEST_REGION_BAD", str(flush))
+    e = _engine(lpg, monkeypatch, m, n + m + 1, defer=K, lib=hooks)
+    monkeypatch.delenv("LPG_TEST_REGION_BAD")
+    assert e.info.region == 1 and e.info.pivot_wg > 0
+    e.generate(n, 17, 0)
+    e.reserve_log(6 * K + 8)
+    e.enqueue(6 * K, 0)
+    res = e.sync()
+    assert e.info.region_recoveries == 1, "the hook's rbad must have stopped a launch"
+    o = Oracle(m, n + m + 1)
+    o.generate(n, 17, 0)
+    ores = o.solve(6 * K, 0)
+    assert res.pivots == ores.pivots == 6 * K and res.objective == ores.objective
+    _assert_same(e, o, m)
+    e.close()
+
+
 @pytest.mark.parametrize("defer", [64, 96])
 @pytest.mark.parametrize("m,n,piv", [(4096, 8192, 300), (2048, 20000, 250)])
 def test_same_as_all_column_kernel(lpg, monkeypatch, m, n, piv, defer):

