@@ -60,13 +60,13 @@ ref:
 phases: tools/probe/liblpg_phases.so
 tools/probe/liblpg_phases.so: $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h $(OBJDIR)/lpg_stamp.o
 	@mkdir -p tools/probe
-	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(OBJDIR)/lpg_stamp.o -ldl
+	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -shared -o $@ $(OBJDIR)/lpg_stamp.o $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip -ldl
 
 # publish / decision-seen stamps of every workgroup only (tools/block_probe.py PHASES_LIB=liblpg_pub.so)
 pub: tools/probe/liblpg_pub.so
 tools/probe/liblpg_pub.so: $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(CSRC)/lpg_internal.h $(CSRC)/lpg_device.h $(OBJDIR)/lpg_stamp.o
 	@mkdir -p tools/probe
-	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -DLPG_PHASES_PUBONLY -shared -o $@ $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip $(OBJDIR)/lpg_stamp.o -ldl
+	$(HIPCC) $(HIPFLAGS) -DLPG_PHASES -DLPG_PHASES_PUBONLY -shared -o $@ $(OBJDIR)/lpg_stamp.o $(CSRC)/lpg_kernels.hip $(CSRC)/lpg_block.hip $(CSRC)/lpg_dual.hip $(CSRC)/lpg_ctx.hip -ldl
 
 asm: $(CSRC)/lpg_kernels.hip
 	$(HIPCC) $(HIPFLAGS) -c --save-temps -o /tmp/lpg_kernels.o $(CSRC)/lpg_kernels.hip

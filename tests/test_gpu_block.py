@@ -94,8 +94,20 @@ def test_to_optimality(lpg, monkeypatch, wg, defer, m, n, seed, kind, rule, trad
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("defer", [15, 16, 17, 31, 33, 47, 48, 49, 63, 64, 65, 79, 80, 81, 95, 96])
-@pytest.mark.parametrize("m,n,seed,kind,rule", [(300, 450, 21, 0, 0), (257, 300, 22, 1, 1)])
+def _edge_cases(defers, keep_slow):
+    """Every block size on the dense Dantzig LP; the KM-style Bland LP (4 s a
+    case: thousands of degenerate pivots) at the bank / batch edges in
+    keep_slow only, the rest `extended` (LPG_EXTENDED_TESTS=1, conftest.py)."""
+    out = []
+    for case in ((300, 450, 21, 0, 0), (257, 300, 22, 1, 1)):
+        for d in defers:
+            slow = case[0] == 257 and d not in keep_slow
+            out.append(pytest.param(d, *case, marks=pytest.mark.extended) if slow else pytest.param(d, *case))
+    return out
+
+
+@pytest.mark.parametrize("defer,m,n,seed,kind,rule",
+                         _edge_cases([15, 16, 17, 31, 33, 47, 48, 49, 63, 64, 65, 79, 80, 81, 95, 96], (16, 17, 64, 65, 96)))
 def test_chain_batch_edges(lpg, monkeypatch, defer, m, n, seed, kind, rule):
     """The chains run in batches of 16 slots (lpg_block.hip chain<>): block
     sizes on either side of every batch edge, dense (Dantzig) and degenerate

@@ -174,9 +174,13 @@ def test_flush_kernels_block_sizes(lpg, monkeypatch, kernel, k, m, n, seed, kind
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("xcd", ["0", "1", "h1", "h2", "h4", "h8"])
-@pytest.mark.parametrize("k", [3, 32, 64, 96, 128])
-@pytest.mark.parametrize("m,n,seed,kind,rule", [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1), (1100, 1300, 17, 0, 1)])
+@pytest.mark.parametrize("xcd,k,m,n,seed,kind,rule", [
+    # the 1100 x 1300 Bland LP at 3-pivot blocks (2.4-9 s a case) with the middle
+    # class counts h1 / h2 / h4 is `extended` (LPG_EXTENDED_TESTS=1): h8 and the
+    # global / grouped queues keep that shape, every other case keeps them all
+    pytest.param(x, k, *lp, marks=pytest.mark.extended if (lp[0] == 1100 and k == 3 and x in ("h1", "h2", "h4")) else ())
+    for lp in [(203, 301, 16, 0, 0), (48, 48, 14, 1, 1), (1100, 1300, 17, 0, 1)]
+    for k in [3, 32, 64, 96, 128] for x in ["0", "1", "h1", "h2", "h4", "h8"]])
 def test_flush_item_maps_agree(lpg, monkeypatch, xcd, k, m, n, seed, kind, rule):
     """k_flushw's global item queue (LPG_FLUSH_XCD=0) and the XCD-grouped
     queues (FlushX: row bands x H column classes, sub-bands, short tail

@@ -255,10 +255,18 @@ def test_processes_big_m_bitwise(lpg, world, m, n, rule, push, mr):
     assert all((p["wg"] > 0) == (push and mr is None) for p in parts)
 
 
-@pytest.mark.parametrize("push,mr", [(False, None), (True, None), (True, "0")])
-@pytest.mark.parametrize("world,m,n,rule,seed,lp", [(2, 257, 300, 0, 9, "gen"), (3, 640, 512, 1, 9, "gen"),
-                                                    (2, 64, 80, 0, 1, "degenerate"), (3, 257, 300, 0, 2, "degenerate"),
-                                                    (2, 300, 200, 1, 3, "degenerate")])
+def _cross(lps, forms, full, default):
+    """Every LP in the default form; the other forms only for the LPs in
+    `full`, the rest `extended` (LPG_EXTENDED_TESTS=1, conftest.py)."""
+    return [pytest.param(*lp, *f, marks=() if (lp in full or f == default) else pytest.mark.extended)
+            for lp in lps for f in forms]
+
+
+@pytest.mark.parametrize("world,m,n,rule,seed,lp,push,mr", _cross(
+    [(2, 257, 300, 0, 9, "gen"), (3, 640, 512, 1, 9, "gen"), (2, 64, 80, 0, 1, "degenerate"),
+     (3, 257, 300, 0, 2, "degenerate"), (2, 300, 200, 1, 3, "degenerate")],
+    [(False, None), (True, None), (True, "0")],
+    full=[(2, 257, 300, 0, 9, "gen"), (3, 257, 300, 0, 2, "degenerate")], default=(True, None)))
 def test_processes_two_phase_bitwise(lpg, world, m, n, rule, seed, lp, push, mr):
     """Two-phase over 2-3 processes (round 3; single rank before): phase I on
     the artificial objective, the |b| test summed over ranks in global row
@@ -280,11 +288,11 @@ def test_processes_dual_bitwise(lpg, world, m, n, seed, defer):
     _processes(world, m, n, seed, push=world == 2, defer=defer, dual=True)   # the push attached: unused, harmless
 
 
-@pytest.mark.parametrize("mr,region", [(None, None), (None, "0"), ("0", None)])
-@pytest.mark.parametrize("world,m,n,kind,rule,defer", [(2, 120, 200, 0, 0, None), (2, 96, 160, 0, 0, "5"),
-                                                       (3, 101, 77, 0, 0, "64"), (2, 64, 64, 1, 1, "5"),
-                                                       (3, 203, 301, 0, 0, "32"), (2, 203, 301, 0, 0, "128"),
-                                                       (2, 1024, 2048, 0, 0, None), (3, 700, 900, 1, 1, "64")])
+@pytest.mark.parametrize("world,m,n,kind,rule,defer,mr,region", _cross(
+    [(2, 120, 200, 0, 0, None), (2, 96, 160, 0, 0, "5"), (3, 101, 77, 0, 0, "64"), (2, 64, 64, 1, 1, "5"),
+     (3, 203, 301, 0, 0, "32"), (2, 203, 301, 0, 0, "128"), (2, 1024, 2048, 0, 0, None), (3, 700, 900, 1, 1, "64")],
+    [(None, None), (None, "0"), ("0", None)],
+    full=[(2, 120, 200, 0, 0, None), (3, 101, 77, 0, 0, "64"), (3, 700, 900, 1, 1, "64")], default=(None, None)))
 def test_processes_owner_push_bitwise(lpg, world, m, n, kind, rule, defer, mr, region):
     """The owner-push exchange between ranks in separate processes sharing the
     GPU (IPC-mapped exchange buffers, the layout of one process per GPU): no

@@ -98,8 +98,18 @@ def test_to_optimality(lpg, monkeypatch, wg, defer, m, n, seed, kind, rule):
     _assert_same(e, o, m)
 
 
-@pytest.mark.parametrize("defer", [16, 17, 63, 64, 65, 80, 95, 96])
-@pytest.mark.parametrize("m,n,seed,kind,rule", [(300, 450, 21, 0, 0), (257, 300, 22, 1, 1)])
+def _edge_cases(defers, keep_slow):
+    """As tests/test_gpu_block.py: the KM-style Bland LP at keep_slow only,
+    the other block sizes `extended` (LPG_EXTENDED_TESTS=1)."""
+    out = []
+    for case in ((300, 450, 21, 0, 0), (257, 300, 22, 1, 1)):
+        for d in defers:
+            slow = case[0] == 257 and d not in keep_slow
+            out.append(pytest.param(d, *case, marks=pytest.mark.extended) if slow else pytest.param(d, *case))
+    return out
+
+
+@pytest.mark.parametrize("defer,m,n,seed,kind,rule", _edge_cases([16, 17, 63, 64, 65, 80, 95, 96], (16, 64, 96)))
 def test_block_size_edges(lpg, monkeypatch, defer, m, n, seed, kind, rule):
     e = _engine(lpg, monkeypatch, m, n + m + 1, defer=defer)
     assert e.info.region == 1
@@ -301,9 +311,12 @@ def test_same_as_all_column_kernel(lpg, monkeypatch, m, n, piv, defer):
         assert np.array_equal(a.get_rows(int(i), 1), b.get_rows(int(i), 1))
 
 
-@pytest.mark.parametrize("xcd", ["0", "1", "h8"])
-@pytest.mark.parametrize("m,n,seed,kind,rule,defer", [(600, 900, 31, 0, 0, 64), (257, 300, 22, 1, 1, 96),
-                                                     (1100, 700, 33, 0, 0, 32)])
+@pytest.mark.parametrize("xcd,m,n,seed,kind,rule,defer", [
+    # the KM-style Bland LP (6-7 s a case) with the grouped queue only; its global
+    # queue and H = 8 classes are `extended` (LPG_EXTENDED_TESTS=1)
+    pytest.param(x, *lp, marks=pytest.mark.extended if (lp[0] == 257 and x != "1") else ())
+    for lp in [(600, 900, 31, 0, 0, 64), (257, 300, 22, 1, 1, 96), (1100, 700, 33, 0, 0, 32)]
+    for x in ["0", "1", "h8"]])
 def test_tile_liveness_map(lpg, monkeypatch, xcd, m, n, seed, kind, rule, defer):
     """The block pass skips tiles without a block-start nonbasic column (tlive,
     built with the region) and loads only the leaving columns' P entries on
