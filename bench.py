@@ -319,7 +319,27 @@ def config5(a):
                          "algorithmic_bytes_per_launch": touched,
                          "full_tableau_bytes_per_launch": eng.info.bytes_per_pivot, "update_ms_mean": upd_ms},
             "status": lpg.STATUS_NAMES.get(res.status, res.status), "pivots_total": res.pivots,
-            "objective": res.objective, "seconds": elapsed}
+            "objective": res.objective, "seconds": elapsed, "build_stamp": lpg_lib.build_stamp}
+    # the whole solve against the oracle's (tests/golden/config5_solve.json), read after the timed region
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    try:
+        import make_config5_golden as G5
+        import trajectory as T
+    finally:
+        sys.path.pop(0)
+    if os.path.exists(G5.FIXTURE):
+        fix = T.load(G5.FIXTURE)
+        ek, er = eng.get_log()
+        line["parity_fixture"] = {
+            "fixture": "tests/golden/config5_solve.json (oracle/liblpo.so, tests/golden/make_config5_golden.py)",
+            "pivots_compared": int(min(len(ek), len(fix["log_k"]))),
+            "identical_log": ek.tolist() == fix["log_k"] and er.tolist() == fix["log_r"],
+            "status": lpg.STATUS_NAMES.get(res.status) == fix["status"],
+            "objective_bits": float(res.objective).hex() == fix["objective_hex"],
+            "basis": T.digest(eng.get_basis()) == fix["basis"],
+            "rows": [T.digest(eng.get_rows(i, 1)[0]) for i in fix["rows"]] == fix["row_digests"]}
+        line["parity_fixture"]["ok"] = all(v for k, v in line["parity_fixture"].items()
+                                           if k not in ("fixture", "pivots_compared"))
     if not a.no_cpu:
         from oracle.lpo import Oracle
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))

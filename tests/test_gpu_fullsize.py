@@ -94,7 +94,32 @@ def test_config3_three_blocks_bitwise(lpg, defer, monkeypatch):
         assert x0[i] == o.get_rows(i, 1)[0, 0]
 
 
+def test_config5_two_phase_against_the_fixture(lpg):
+    """Config 5's whole two-phase solve against tests/golden/config5_solve.json
+    (the C oracle's solve, made in the build container by
+    tests/golden/make_config5_golden.py): status, pivot count, objective
+    bits, the whole log, basis, column 0 and 67 sampled rows (digests)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import trajectory as T
+    from make_config5_golden import ART_FIRST, CAP, FIXTURE, M, N, SEED as S5
+    sys.path.pop(0)
+    fix = T.load(FIXTURE)
+    e = lpg.Engine(M, N + M + 1)
+    e.generate(N, S5, lpg.GEN_ARTIFICIAL)
+    e.reserve_log(CAP + 8)
+    res = e.solve_two_phase(ART_FIRST, None, CAP, lpg.RULE_BLAND)
+    k, r = e.get_log()
+    assert res.status_name == fix["status"] == "OPTIMAL" and res.pivots == fix["pivots"] > 4096
+    assert float(res.objective).hex() == fix["objective_hex"]
+    assert k.tolist() == fix["log_k"] and r.tolist() == fix["log_r"]
+    assert T.digest(e.get_basis()) == fix["basis"] and T.digest(e.get_column0()) == fix["column0"]
+    assert [T.digest(e.get_rows(i, 1)[0]) for i in fix["rows"]] == fix["row_digests"]
+
+
+@pytest.mark.extended
 def test_config5_two_phase_full_bitwise(lpg):
+    """The same against the oracle run live on the GPU box's cores (~45 s)."""
     m = n = 8192
     art_first = 1 + n + (m + 1) // 2
     cap = 20000

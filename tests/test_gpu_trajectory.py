@@ -96,3 +96,35 @@ def test_config3_bench_trajectory_bitwise(fix, defer, monkeypatch):
     out = T.compare(fix, k, r, {T.PIVOTS: snap})
     assert out["log_equal"], f"first differing pivot: {out['first_mismatch']}"
     assert out["pivots_compared"] == T.PIVOTS and out["ok"], out
+
+
+def _config5():
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    try:
+        import make_config5_golden as G5
+    finally:
+        sys.path.pop(0)
+    return G5, T.load(G5.FIXTURE)
+
+
+def test_config5_fixture_shape():
+    G5, fix = _config5()
+    assert fix["status"] == "OPTIMAL" and fix["pivots"] == len(fix["log_k"]) == len(fix["log_r"]) > 4096
+    assert fix["m"] == G5.M and fix["n"] == G5.N and fix["art_first"] == G5.ART_FIRST
+    assert fix["rows"] == G5.sample_rows() and len(fix["row_digests"]) == len(fix["rows"])
+
+
+@pytest.mark.slow_cpu
+def test_config5_fixture_first_pivots_are_the_oracle():
+    """The oracle's first 160 pivots of the same two-phase solve (a capped
+    run: the log is a prefix of the full one) equal the fixture's."""
+    from oracle.lpo import GEN_ARTIFICIAL, RULE_BLAND, Oracle
+    G5, fix = _config5()
+    o = Oracle(G5.M, G5.N + G5.M + 1, nthreads=min(8, os.cpu_count() or 1))
+    try:
+        o.generate(G5.N, G5.SEED, GEN_ARTIFICIAL)
+        o.solve_two_phase(G5.ART_FIRST, None, 160, RULE_BLAND)
+        k, r = o.get_log()
+    finally:
+        o.close()
+    assert len(k) == 160 and k.tolist() == fix["log_k"][:160] and r.tolist() == fix["log_r"][:160]
