@@ -403,12 +403,28 @@ def main():
         raise SystemExit("no GPU visible")
     dev = local % ndev
 
+    host_comm = [a.host_comm]
+
     def make_engine(push):
         e = lpg.Engine(m, n + m + 1, device=dev, world=world, rank=rank)
-        if world > 1 and not a.host_comm:
-            uid = [lpg.Engine.rccl_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            e.comm_init_rccl(uid[0])
+        if world > 1 and not host_comm[0]:
+            # RCCL for setup (and the collectives); if its init fails on any rank
+            # (an error, not a hang), every rank rebuilds on the gloo host collectives
+            ok = True
+            try:
+                uid = [lpg.Engine.rccl_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(uid, src=0)
+                e.comm_init_rccl(uid[0])
+            except lpg.LPGError as ex:
+                print(f"bench: rank {rank}: RCCL communicator failed ({ex}); using the host collectives",
+                      file=sys.stderr)
+                ok = False
+            t = torch.tensor([1 if ok else 0], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            if not t.item():
+                e.close()
+                host_comm[0] = True
+                return make_engine(push)
         elif world > 1 or a.force_push:
             e.comm_init_host(*host_ops(world))
         elif a.force_rccl:
@@ -582,7 +598,8 @@ def main():
                    "parallelism": f"row-block x{world}" + (
                        (" (owner push per pivot: pivot row and candidates stored into IPC-mapped peer buffers"
                         + (", uncached" if info.exchange == 2 else "") + ")"
-                        if use_push else " (RCCL allgather + allreduce per pivot)")
+                        if use_push else (" (host gloo allgather + allreduce per pivot)" if host_comm[0]
+                                          else " (RCCL allgather + allreduce per pivot)"))
                        if world > 1 or a.force_rccl or a.force_push else ""),
                    "update": (f"deferred blocks of {defer} pivots (one k_flush pass per block)" if defer
                               else "eager rank-1 update per pivot"),

@@ -45,6 +45,29 @@ def test_fixture_shape(fix):
     assert all(b >= a for a, b in zip(z, z[1:])), "z must not decrease (a maximisation)"
 
 
+def test_compare_finds_a_changed_pivot_and_a_changed_bit(fix):
+    """The checker itself: a swapped pivot is reported at its index, one
+    flipped bit in a checkpoint's rows fails that field only."""
+    k, r = np.array(fix["log_k"]), np.array(fix["log_r"])
+    assert T.compare(fix, k, r, {})["ok"]
+    k2 = k.copy()
+    k2[1700] += 1
+    out = T.compare(fix, k2, r, {})
+    assert not out["ok"] and out["first_mismatch"] == 1700
+    snap = dict(fix["checkpoints"]["2400"])
+    assert T.compare(fix, k, r, {2400: snap})["ok"]
+    rows = list(snap["rows"])
+    rows[3] = "0" * 64
+    out = T.compare(fix, k, r, {2400: dict(snap, rows=rows)})
+    assert not out["ok"] and out["checkpoints"]["2400"] == {"objective_hex": True, "basis": True, "column0": True,
+                                                            "objective_row": True, "rows": False}
+    # a digest is of the little-endian bytes: one ulp changes it
+    a = np.linspace(0.0, 1.0, 9)
+    b = a.copy()
+    b[4] = np.nextafter(b[4], 2.0)
+    assert T.digest(a) != T.digest(b) and T.digest(a) == T.digest(a.copy())
+
+
 @pytest.mark.slow_cpu
 def test_fixture_first_block_is_the_oracle(fix):
     """Recompute pivots 1..96 with the oracle on this host's cores (~30 s and
