@@ -62,17 +62,34 @@ def spawn_ranks_if_needed() -> None:
     n = ap.parse_known_args()[0].gpus
     if n <= 1:
         return
+    import ctypes
+    import signal
     import subprocess
     import tempfile
     tmp = tempfile.mkdtemp(prefix="lpg_bench_")
     out_path = os.path.join(tmp, "rank0.out")
     procs = []
+
+    def die_with_parent():            # in the child, before exec: no rank outlives this launcher
+        try:
+            ctypes.CDLL(None).prctl(1, signal.SIGKILL)    # PR_SET_PDEATHSIG
+        except Exception:
+            pass
+
+    def stop(signum, frame):          # a time limit on this launcher ends the ranks too
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        raise SystemExit(128 + signum)
+
+    signal.signal(signal.SIGTERM, stop)
+    signal.signal(signal.SIGINT, stop)
     with open(out_path, "wb") as out0:
         for r in range(n):
             env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                        MASTER_ADDR="127.0.0.1", LPG_BENCH_INIT_FILE=os.path.join(tmp, "rendezvous"))
             procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                          stdout=out0 if r == 0 else subprocess.DEVNULL))
+                                          stdout=out0 if r == 0 else subprocess.DEVNULL, preexec_fn=die_with_parent))
     rc = 0
     while any(p.poll() is None for p in procs):
         bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
