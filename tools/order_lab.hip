@@ -175,6 +175,9 @@ int main(int argc, char **argv) {
             for (long ir : {16L, 64L, 128L, 256L, 1024L, 2048L}) {
                 if (ord == 1 && ir > rows / 8) continue;
                 if (ord < 4 && getenv("LAB_ORD4_ONLY")) continue;
+                // LAB_ORD=o LAB_IR=r: one configuration only (for rocprofv3 --pmc passes)
+                if (getenv("LAB_ORD") && atoi(getenv("LAB_ORD")) != ord) continue;
+                if (getenv("LAB_IR") && atol(getenv("LAB_IR")) != ir) continue;
                 auto k = ord == 0 ? k_order_rmw<0> : ord == 1 ? k_order_rmw<1> : ord == 2 ? k_order_rmw<2>
                        : ord == 3 ? k_order_rmw<3> : k_order_rmw<4>;
                 std::vector<float> t;

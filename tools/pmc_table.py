@@ -29,7 +29,8 @@ def means(tags):
                               recursive=True):
             with open(path) as f:
                 for row in csv.DictReader(f):
-                    per[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                    kn = row["Kernel_Name"][:80] if os.environ.get("FULLNAME") else short(row["Kernel_Name"])
+                    per[kn][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return {k: {c: (sum(v) / len(v), len(v)) for c, v in d.items()} for k, d in per.items()}
 
 
@@ -57,7 +58,7 @@ def main():
     for k in sorted(m, key=lambda k: -max((v[0] for v in m[k].values()), default=0)):
         print(k, {c: round(v[0], 1) for c, v in sorted(m[k].items())}, "dispatches",
               max(v[1] for v in m[k].values()))
-        if k in ("k_flushw", "k_pivot_block"):
+        if k in ("k_flushw", "k_pivot_block") or "flushw" in k:
             for c, v in derived(m[k]).items():
                 print(f"    {c}: {v:.3f}")
 
