@@ -6,12 +6,14 @@
 //           A operands still read from LDS)
 //   MODE 2  no tableau traffic: the matrix path alone (multiplier ring, LDS,
 //           barrier, MFMAs; stores only under a never-true condition)
+//   MODE 3  MODE 0 with buffer loads / stores predicated by their bounds (no
+//           VMEM op behind an exec branch; checked bitwise too)
 // over config 3's shape (16384 rows, 49153 columns, pitch 49216, the 32769
 // first columns live, P zero beyond), random data, 96 pending slots, the
 // product's XCD item map (flushx_plan). Run the probes under rocprofv3 --pmc
 // too (LAB_MODE=m selects one).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o tools/flushw_probe tools/flushw_probe.hip
-//   tools/flushw_probe [reps]
+//   tools/flushw_probe [reps]        (LAB_TS=1: per-item timestamps of MODE 0 / 2 as well)
 #include "../linearprogramming_amd/csrc/lpg_kernels.hip"
 
 #include <stdio.h>
@@ -31,6 +33,12 @@
     } while (0)
 
 namespace lpg {
+
+// LAB_TS=1: per-item timestamps of k_flushw_probe (s_memrealtime, 100 MHz):
+// block b's record r = {start, end, tile, rows}; record kTsMax = {kernel entry,
+// exit, items, 0}
+constexpr int kTsMax = 96;
+__device__ unsigned long long *g_ts = nullptr;
 
 template <int KMAX, int NB, int LB, int WPB, int MODE>
 __global__ __launch_bounds__(64 * WPB, LB) void k_flushw_probe(double *__restrict__ T, Geo g, DevState *__restrict__ st,
@@ -58,8 +66,12 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw_probe(double *__restric
     unsigned long long touched = 0;
     const int g0 = (int)(blockIdx.x & 7);   // blocks with the same b % 8 share an XCD
     int gd = 0;                             // X.on: queue g0 + gd (mod 8) is being drained
+    unsigned long long *ts = g_ts ? g_ts + (size_t)blockIdx.x * (kTsMax + 1) * 4 : nullptr;
+    int nrec = 0;
+    if (ts && threadIdx.x == 0) ts[kTsMax * 4] = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         __syncthreads();
+        if (ts && threadIdx.x == 0 && nrec > 0 && nrec <= kTsMax) ts[(nrec - 1) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
         if (threadIdx.x == 0) {
             if (X.on) {
                 int64_t it = -1;
@@ -89,6 +101,12 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw_probe(double *__restric
             if (item >= nitems) break;
             flush_item(item, ntiles, rows, g.nloc, tile, i0, i1);
         }
+        if (ts && threadIdx.x == 0 && nrec < kTsMax) {
+            ts[nrec * 4] = __builtin_amdgcn_s_memrealtime();
+            ts[nrec * 4 + 2] = (unsigned long long)tile;
+            ts[nrec * 4 + 3] = (unsigned long long)(i1 - i0);
+        }
+        nrec++;
         // region mode (launch_flush_main): a tile without block-start nonbasic
         // columns holds live entries only in a leaving column of the block, if
         // any (one whose trade did not move it); otherwise it is skipped
@@ -139,6 +157,27 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw_probe(double *__restric
             touched += (unsigned long long)sum * (unsigned long long)(i1 - i0);
         }
         const int nb = (int)((i1 - i0 + 15) / 16);
+        // MODE 3: the tableau and multiplier traffic as buffer loads / stores
+        // whose bounds do the predication (rows past i1 and dead lanes out of
+        // range: loads return 0, stores are dropped), so no VMEM op sits behind
+        // an exec branch and the compiler can count vmcnt exactly (with the
+        // branches every band ended on vmcnt(0): the band's stores and the
+        // next band's loads drained before the next barrier)
+        const int64_t i0u = ((int64_t)__builtin_amdgcn_readfirstlane((int)(i0 >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int)i0);
+        const int64_t i1u = ((int64_t)__builtin_amdgcn_readfirstlane((int)(i1 >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int)i1);
+        int voff[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) voff[r] = ok ? (int)(((int64_t)(lk + 4 * r) * ld + cl) * 8) : (int)0x80000000u;
+        auto trs = [&](int s) {
+            const int64_t row0 = i0u + 16 * s;
+            int64_t nr = i1u - row0;
+            nr = nr < 0 ? 0 : nr > 16 ? 16 : nr;
+            return __builtin_amdgcn_make_buffer_rsrc((void *)(T + row0 * ld), 0, (int)(nr * ld * 8), 0x00020000);
+        };
+        const __amdgpu_buffer_rsrc_t crs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)Cbuf, 0, (int)((int64_t)np * cs * 8), 0x00020000);
         // multiplier piece e of band s: slot q = e / 8, band rows 2 (e % 8) .. +1
         // (zeros past np and past i1: A = -0 there, x + -0 == x)
         auto cload = [&](d2 (&cr)[PER], int s) {
@@ -148,15 +187,18 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw_probe(double *__restric
                 const int q = e >> 3, rr = 2 * (e & 7);
                 const int64_t row = i0 + 16 * s + rr;
                 d2 v = d2{0.0, 0.0};
-                if (s < nb && q < np && row < i1 && (NPC % NTH == 0 || e < NPC))
+                if (MODE == 3)   // q >= np out of range (0); rows past i1 feed only rows that are not stored
+                    v = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(crs, (int)(((int64_t)q * cs + row) * 8), 0, 0));
+                else if (s < nb && q < np && row < i1 && (NPC % NTH == 0 || e < NPC))
                     v = *(const d2 *)(Cbuf + (int64_t)q * cs + row);   // row + 1 < cs
-                cr[u] = -v;
+                cr[u] = MODE == 3 ? v : -v;   // MODE 3 negates at the LDS store (a wait there anyway)
             }
         };
         auto cstore = [&](const d2 (&cr)[PER], int s) {
 #pragma unroll
             for (int u = 0; u < PER; u++)
-                if (NPC % NTH == 0 || threadIdx.x + u * NTH < NPC) *(d2 *)(&sC[s % NB][2 * (threadIdx.x + u * NTH)]) = cr[u];
+                if (NPC % NTH == 0 || threadIdx.x + u * NTH < NPC)
+                    *(d2 *)(&sC[s % NB][2 * (threadIdx.x + u * NTH)]) = MODE == 3 ? -cr[u] : cr[u];
         };
         for (int s = 0; s < NB - 1; s++) {   // prologue: bands 0 .. NB-2 into the ring
             d2 cr[PER];
@@ -166,6 +208,12 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw_probe(double *__restric
         d2 cn[PER];
         cload(cn, NB - 1);
         auto tload = [&](d2 (&x)[4], int s) {
+            if (MODE == 3) {
+                const __amdgpu_buffer_rsrc_t rs = trs(s);
+#pragma unroll
+                for (int r = 0; r < 4; r++) x[r] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff[r], 0, 2));
+                return;
+            }
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int64_t row = i0 + 16 * s + lk + 4 * r;
@@ -177,10 +225,11 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw_probe(double *__restric
         tload(t, 0);
         for (int s = 0; s < nb; s++) {
             d2 tn[4];                         // one band ahead (two ahead measured no faster)
-            if (s + 1 < nb) tload(tn, s + 1);
+            if (MODE == 3 || s + 1 < nb) tload(tn, s + 1);
             __syncthreads();                  // band s is staged; ring slot (s - 1) % NB is free
             cstore(cn, s + NB - 1);
             cload(cn, s + NB);
+            d2 tout[4] = {t[0], t[1], t[2], t[3]};
             if (wlive) {
                 d4 ae = d4{t[0].x, t[1].x, t[2].x, t[3].x};
                 d4 ao = d4{t[0].y, t[1].y, t[2].y, t[3].y};
@@ -212,16 +261,34 @@ __global__ __launch_bounds__(64 * WPB, LB) void k_flushw_probe(double *__restric
                     a0 = n0;
                     a1 = n1;
                 }
+                if (MODE != 3) {
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int64_t row = i0 + 16 * s + lk + 4 * r;
-                    if (ok && row < i1 && (MODE != 2 || ae[r] == 12345.0))
-                        __builtin_nontemporal_store(d2{ae[r], ao[r]}, (d2 *)(T + row * ld + cl));
+                    for (int r = 0; r < 4; r++) {
+                        const int64_t row = i0 + 16 * s + lk + 4 * r;
+                        if (ok && row < i1 && (MODE != 2 || ae[r] == 12345.0))
+                            __builtin_nontemporal_store(d2{ae[r], ao[r]}, (d2 *)(T + row * ld + cl));
+                    }
+                } else {
+                    tout[0] = d2{ae[0], ao[0]};
+                    tout[1] = d2{ae[1], ao[1]};
+                    tout[2] = d2{ae[2], ao[2]};
+                    tout[3] = d2{ae[3], ao[3]};
                 }
+            }
+            if (MODE == 3) {   // unconditional: a dead wave's lanes are all out of range
+                const __amdgpu_buffer_rsrc_t rs = trs(s);
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, tout[r]), rs, voff[r], 0, 2);
             }
 #pragma unroll
             for (int r = 0; r < 4; r++) t[r] = tn[r];
         }
+    }
+    if (ts && threadIdx.x == 0) {
+        if (nrec > 0 && nrec <= kTsMax) ts[(nrec - 1) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+        ts[kTsMax * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+        ts[kTsMax * 4 + 2] = (unsigned long long)nrec;
     }
     if (threadIdx.x == 0 && touched) atomicAdd(&st->touched, touched);
 }
@@ -514,6 +581,10 @@ int main(int argc, char **argv) {
             hipLaunchKernelGGL((k_flushw2_probe<96, 2, 1, 8, M, S>), dim3(grid), dim3(512), 0, 0, T, g, st, Pbuf, Cbuf, \
                                cs, ntiles, nitems, rows, 1, X, (const int32_t *)nullptr, (const int64_t *)nullptr,    \
                                (const int32_t *)nullptr);
+        else if (which == 9)
+            hipLaunchKernelGGL((k_flushw_probe<96, 2, 1, 8, 3>), dim3(grid), dim3(512), 0, 0, T, g, st, Pbuf, Cbuf, cs,
+                               ntiles, nitems, rows, 1, X, (const int32_t *)nullptr, (const int64_t *)nullptr,
+                               (const int32_t *)nullptr);
         LPG_FW2(4, 0, 2)
         LPG_FW2(5, 1, 2)
         LPG_FW2(6, 2, 2)
@@ -536,13 +607,14 @@ int main(int argc, char **argv) {
            "probe MODE 0 vs lpg::k_flushw: %llu doubles differ\n", (long long)m, (long long)ncols, (long long)ld, K,
            (long long)nstruct, X.H, X.rb, X.rs, hb);
     if (hb) return 1;
-    for (int w : {4, 7}) {
+    for (int w : {4, 7, 9}) {
         CHK(hipMemcpy(T, T0, n * 8, hipMemcpyDeviceToDevice));
         launch(w);
         CHK(hipMemset(bad, 0, 8));
         hipLaunchKernelGGL(k_diff, dim3(4096), dim3(256), 0, 0, T, Tr, n, bad);
         CHK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
-        printf("# %d-row bands vs lpg::k_flushw: %llu doubles differ\n", w == 4 ? 32 : 64, hb);
+        if (w == 9) printf("# MODE 3 (buffer ops) vs lpg::k_flushw: %llu doubles differ\n", hb);
+        else printf("# %d-row bands vs lpg::k_flushw: %llu doubles differ\n", w == 4 ? 32 : 64, hb);
         if (hb) return 1;
     }
     hipEvent_t e0, e1;
@@ -551,11 +623,13 @@ int main(int argc, char **argv) {
     const char *names[] = {"lpg::k_flushw<96,2,1,8> (product)", "probe MODE 0 (same body)",
                            "probe MODE 1 (no MFMA: memory path)", "probe MODE 2 (no T traffic: matrix path)",
                            "32-row bands MODE 0", "32-row bands MODE 1 (memory path)",
-                           "32-row bands MODE 2 (matrix path)", "64-row bands MODE 0", "64-row bands MODE 2 (matrix path)"};
+                           "32-row bands MODE 2 (matrix path)", "64-row bands MODE 0", "64-row bands MODE 2 (matrix path)",
+                           "probe MODE 3 (buffer ops, no VMEM branches)"};
     const int only = getenv("LAB_MODE") ? atoi(getenv("LAB_MODE")) : -1;
     for (int round = 0; round < 2; round++)
-        for (int w = 0; w < 9; w++) {
+        for (int w = 0; w < 10; w++) {
             if (only >= 0 && w != only) continue;
+            if (only == -2 && w != 0 && w != 1 && w != 9) continue;
             std::vector<float> t;
             for (int r = 0; r <= reps; r++) {
                 CHK(hipMemcpy(T, T0, n * 8, hipMemcpyDeviceToDevice));
@@ -572,5 +646,59 @@ int main(int argc, char **argv) {
                    bytes / (t[0] * 1e-3) / 1e9, flops / (t[0] * 1e-3) / 1e12);
             fflush(stdout);
         }
+    if (getenv("LAB_TS")) {
+        // per-item timestamps of probe MODE 0 and MODE 2 (the last item's end
+        // includes its final barrier; the dequeue of a queue past its end is
+        // the "item" with rows = 0 that ends the block)
+        unsigned long long *dts;
+        const size_t nts = (size_t)grid * (kTsMax + 1) * 4;
+        CHK(hipMalloc(&dts, nts * 8));
+        CHK(hipMemcpyToSymbol(HIP_SYMBOL(g_ts), &dts, sizeof dts));
+        std::vector<unsigned long long> h(nts);
+        for (int w : {1, 3, 9}) {
+            for (int rep = 0; rep < 3; rep++) {
+                CHK(hipMemset(dts, 0, nts * 8));
+                CHK(hipMemcpy(T, T0, n * 8, hipMemcpyDeviceToDevice));
+                launch(w);
+                CHK(hipDeviceSynchronize());
+                CHK(hipMemcpy(h.data(), dts, nts * 8, hipMemcpyDeviceToHost));
+                unsigned long long k0 = ~0ull, k1 = 0;
+                for (unsigned b = 0; b < grid; b++) {
+                    const unsigned long long *r = &h[(size_t)b * (kTsMax + 1) * 4];
+                    k0 = std::min(k0, r[kTsMax * 4]);
+                    k1 = std::max(k1, r[kTsMax * 4 + 1]);
+                }
+                const double span = (k1 - k0) * 0.01;   // us
+                double live = 0, dead = 0, head = 0, tail = 0, gaps = 0;
+                std::vector<double> exits;
+                int nlive = 0, ndead = 0, nshort = 0;
+                double tshort = 0;
+                for (unsigned b = 0; b < grid; b++) {
+                    const unsigned long long *r = &h[(size_t)b * (kTsMax + 1) * 4];
+                    const int nr = (int)std::min<unsigned long long>(r[kTsMax * 4 + 2], kTsMax);
+                    head += (r[0] - r[kTsMax * 4]) * 0.01;
+                    exits.push_back((k1 - r[kTsMax * 4 + 1]) * 0.01);
+                    for (int i = 0; i < nr; i++) {
+                        const double d = (r[i * 4 + 1] - r[i * 4]) * 0.01;
+                        if (i > 0) gaps += (r[i * 4] - r[(i - 1) * 4 + 1]) * 0.01;
+                        const bool isdead = r[i * 4 + 2] > (unsigned long long)(nstruct / 256);
+                        if (r[i * 4 + 3] == 0) continue;
+                        if (isdead) { dead += d; ndead++; }
+                        else { live += d; nlive++; if (r[i * 4 + 3] < 2048) { nshort++; tshort += d; } }
+                    }
+                    tail += (k1 - r[kTsMax * 4 + 1]) * 0.01;
+                }
+                std::sort(exits.begin(), exits.end());
+                const double tot = span * grid;
+                printf("# ts %-40s span %.1f us: live items %d (%.1f%% of block-time, %d short ones %.1f us avg), "
+                       "dead tiles %d (%.2f%%), head %.2f%%, gaps %.2f%%, idle after exit %.2f%% "
+                       "(exit-to-end: min %.1f median %.1f max %.1f us)\n",
+                       names[w], span, nlive, 100 * live / tot, nshort, nshort ? tshort / nshort : 0.0, ndead,
+                       100 * dead / tot, 100 * head / tot, 100 * gaps / tot, 100 * tail / tot, exits[0],
+                       exits[exits.size() / 2], exits.back());
+                fflush(stdout);
+            }
+        }
+    }
     return 0;
 }
