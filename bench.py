@@ -23,8 +23,12 @@ pivots (the kernel and K named in `roofline`).
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
 With N > 1 the tableau is row-block partitioned over N processes (one per
-GPU); per pivot the ranks allgather the ratio candidates and allreduce the
-pivot row over RCCL (strong scaling: the LP is the same for every N).
+GPU; strong scaling: the LP is the same for every N). Per pivot the owner of
+the pivot row stores it, with the ratio candidates, into every peer's
+IPC-mapped exchange buffer (the owner push, default); `--exchange rccl`
+allgathers the candidates and allreduces the pivot row over RCCL instead, and
+the bench falls back to those collectives (or to gloo host collectives when
+RCCL cannot start) if the push cannot attach or fails in the warm-up.
 
 Rank 0 prints ONE JSON line. `roofline.achieved` = algorithmic bytes of one
 launch of the dominant kernel on rank 0 (k_flushw: 16 B x local constraint
