@@ -301,7 +301,7 @@ struct FlushX {
     int32_t rs;       // sub-band rows (multiple of 16, <= rb)
     int32_t tt;       // tail tiles per group
     int32_t on;
-    int32_t pad;
+    int32_t tq;       // row pieces per tail tile (flushx_plan: 8; 0 reads as 4)
 };
 struct FlushXGroup {
     int64_t r0, r1, ntg, nsb, ttg, nq, qrows, count;
@@ -315,7 +315,8 @@ __host__ __device__ inline FlushXGroup flushx_group(const FlushX &f, int g) {
     if (o.r0 >= f.nloc || o.ntg == 0) return o;
     o.nsb = (o.r1 - o.r0 + f.rs - 1) / f.rs;
     const int64_t ls = (o.r1 - o.r0) - (o.nsb - 1) * f.rs;   // last sub-band's rows
-    o.qrows = ((ls + 3) / 4 + 15) / 16 * 16;
+    const int64_t tq = f.tq > 0 ? f.tq : 4;
+    o.qrows = ((ls + tq - 1) / tq + 15) / 16 * 16;
     o.nq = (ls + o.qrows - 1) / o.qrows;
     o.ttg = f.tt < o.ntg ? f.tt : o.ntg;
     o.count = (o.nsb - 1) * o.ntg + (o.ntg - o.ttg) + o.nq * o.ttg;

@@ -2603,7 +2603,8 @@ static int64_t env_range(const char *name, int64_t lo, int64_t hi) {   // 0 when
 // default 2048): the most column classes H whose bands fit, so P is re-read
 // by 8 / H bands (one P tile read per band: the tile's pieces run back to
 // back); bands that do not fit at H = 1 are swept in sub-bands that do. The
-// tail: two rounds of short items per group's blocks (LPG_FLUSH_XTAIL tiles).
+// tail: two rounds of short items per group's blocks (LPG_FLUSH_XTAIL tiles,
+// LPG_FLUSH_XPIECES row pieces each).
 // xcd: -1 auto (tableaus of >= 1024 rows and >= 64 tiles), 0 off (the global
 // queue, flush_item), 1 on at any size, 10 + H on with H column classes (tests).
 static FlushX flushx_plan(int64_t ntiles, int64_t nloc, int kmax, int64_t nblocks, int xcd) {
@@ -2611,6 +2612,7 @@ static FlushX flushx_plan(int64_t ntiles, int64_t nloc, int kmax, int64_t nblock
     if (xcd == 0 || nloc < 1 || ntiles < 1 || (xcd < 0 && (nloc < 1024 || ntiles < 64))) return X;
     static const int64_t cb = env_range("LPG_FLUSH_CB", 256, 65536) * 1024;
     static const int64_t ttf = env_range("LPG_FLUSH_XTAIL", 1, 1 << 20);
+    static const int64_t tqf = env_range("LPG_FLUSH_XPIECES", 1, 64);
     const int64_t budget = cb ? cb : (int64_t)2048 * 1024;
     auto band = [&](int H) { return ((nloc + 8 / H - 1) / (8 / H) + 15) / 16 * 16; };
     int H = 1;
@@ -2630,6 +2632,10 @@ static FlushX flushx_plan(int64_t ntiles, int64_t nloc, int kmax, int64_t nblock
     X.rb = (int32_t)rb;
     X.rs = (int32_t)std::min<int64_t>(rb, ((rb + nsb - 1) / nsb + 15) / 16 * 16);
     X.tt = (int32_t)(ttf ? ttf : std::max<int64_t>(1, nblocks / 8 / 2));
+    // eighth-height pieces: config 3 pass 2.130 -> 2.100 ms, config 5 0.192 -> 0.170 ms,
+    // config 4 flat (16 / 32 pieces lose at config 5; fewer tail tiles cost config 5,
+    // whose live columns sit in a few low tiles, a third; profiles/r06_ab_flush_pieces.log)
+    X.tq = (int32_t)(tqf ? tqf : 8);
     X.on = 1;
     return X;
 }

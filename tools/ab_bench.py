@@ -33,9 +33,12 @@ def main():
             d = json.loads(p.stdout.strip().splitlines()[-1])
             roof = d["roofline"]
             tr = d.get("parity_trajectory") or {}
+            mf = (roof.get("mfma") or {}).get("achieved", float("nan"))
+            hb = (roof.get("hbm") or {}).get("achieved", float("nan"))
+            fx = (d.get("parity_fixture") or {}).get("ok")
             print(f"rep {rep} [{v or 'default'}] {d['value']:.0f} pivots/s  {d['ms_per_step']:.3f} ms/block  "
-                  f"pass {roof['update_ms_mean']:.3f} ms  {roof['mfma']['achieved']:.1f} TFLOP/s  "
-                  f"HBM {roof['hbm']['achieved']:.0f} GB/s  trajectory_ok={tr.get('ok')}", flush=True)
+                  f"pass {roof.get('update_ms_mean', float('nan')):.3f} ms  {mf:.1f} TFLOP/s  "
+                  f"HBM {hb:.0f} GB/s  trajectory_ok={tr.get('ok')} fixture_ok={fx}", flush=True)
 
 
 if __name__ == "__main__":
