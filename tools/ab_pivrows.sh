@@ -1,4 +1,6 @@
 #!/bin/bash
+# (LPG_PIVROWS and k_flush_pivot_rows_pf existed only for this experiment; the source was
+# reverted after it: DESIGN.md §8, profiles/r06_ab_pivrows_pf.log)
 # Round 6: the latency-hidden pivot-row rewrite (k_flush_pivot_rows_pf,
 # default) against the form before (LPG_PIVROWS=0), interleaved, config 3
 # (driver's form) and config 4; then rocprofv3 kernel stats of both at config 3.
